@@ -1,0 +1,119 @@
+// Integer-VALU peak microbenchmark for gfx950 (MI355X).
+// Measures the sustained rate of the instructions the BLS12-381 field
+// arithmetic is built from: v_mad_u64_u32 (32x32+64 -> 64 MAC),
+// v_add_co_u32 / v_addc_co_u32 (carry chain) and v_mul_lo/hi_u32.
+// The measured v_mad_u64_u32 rate is the roofline denominator reported by
+// bench.py (DESIGN.md "Roofline"). Each thread runs 8 independent chains so
+// the SIMD is issue-bound, not latency-bound.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+constexpr int ITERS = 4096;
+
+__global__ __launch_bounds__(256) void k_mad64(uint64_t* out, uint32_t seed) {
+  uint32_t a = seed + threadIdx.x, b = seed * 3u + blockIdx.x;
+  uint64_t acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = (uint64_t)(a + k) << 7;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint64_t cy;
+      asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(cy) : "v"(a), "v"(b));
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= acc[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_addc(uint64_t* out, uint32_t seed) {
+  uint32_t a = seed + threadIdx.x;
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { lo[k] = a + k; hi[k] = a ^ k; }
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // one v_add_co_u32 + one v_addc_co_u32 per step: 2 VALU ops
+      asm volatile("v_add_co_u32 %0, vcc, %0, %2\n\tv_addc_co_u32 %1, vcc, %1, %2, vcc"
+                   : "+v"(lo[k]), "+v"(hi[k]) : "v"(a) : "vcc");
+    }
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= ((uint64_t)hi[k] << 32) | lo[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_mullo(uint64_t* out, uint32_t seed) {
+  uint32_t a = seed + threadIdx.x;
+  uint32_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = a + k;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[k]) : "v"(a));
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void k_add(uint64_t* out, uint32_t seed) {
+  uint32_t a = seed + threadIdx.x;
+  uint32_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = a + k;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("v_add_u32 %0, %0, %1" : "+v"(x[k]) : "v"(a));
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <typename K>
+static double time_kernel(K kern, uint64_t* d, int blocks, int reps) {
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, 1u);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, (uint32_t)r);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms = 0; CHECK(hipEventElapsedTime(&ms, e0, e1));
+  return ms / reps;
+}
+
+int main() {
+  hipDeviceProp_t p; CHECK(hipGetDeviceProperties(&p, 0));
+  const int cus = p.multiProcessorCount;
+  const int blocks = cus * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU
+  uint64_t* d; CHECK(hipMalloc(&d, (size_t)blocks * 256 * 8));
+  const double lanes = (double)blocks * 256.0;
+  const double ops = lanes * ITERS * 8.0;
+  double t;
+  printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d", p.gcnArchName, cus, p.clockRate);
+  t = time_kernel(k_mad64, d, blocks, 5);
+  printf(", \"v_mad_u64_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_addc, d, blocks, 5);
+  printf(", \"v_add_co+v_addc_co_Tops\": %.3f", 2.0 * ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_mullo, d, blocks, 5);
+  printf(", \"v_mul_lo_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_add, d, blocks, 5);
+  printf(", \"v_add_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  printf("}\n");
+  CHECK(hipFree(d));
+  return 0;
+}
