@@ -1,0 +1,276 @@
+"""Benchmark: BLS signature verifications/s on MI355X (BASELINE.json `metric`).
+
+Workload (BASELINE.json configs[1]): 2^16 independent
+`bls_verify` deposit proof-of-possession checks -- random secret keys, random
+32-byte messages, domain = bls_domain(DOMAIN_DEPOSIT) = 3 -- with 1/16 of the
+items tampered (message bit flip or signature swap: full work, verdict False).
+One step = one `bls381_verify_batch_device` over the whole batch (decode G1 +
+subgroup, decode G2 + subgroup, hash_to_G2, 2-pair Miller loop, final
+exponentiation, verdict), inputs resident in HBM.
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank verifies its
+own 2^16 batch (independent items shard with no data-path collective; weak
+scaling); barrier + synchronize around the timed steps, max over ranks.
+
+Also reported: committee pubkey aggregation (C3 shape: 1024 committees x 128
+pubkeys), the dominant kernel's roofline against the measured v_mad_u64_u32
+peak, and a CPU baseline (the oracle's py_ecc-algorithm restatement on the
+host cores, bounded sample of the same items).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
+
+VALU_PEAK_FILE = os.path.join(ROOT, "profiles", "valu_peak_r01.json")
+MACS_PER_FP_MUL = 300   # 12-limb no-carry CIOS: 144 + 144 v_mad_u64_u32 + 12 v_mul_lo_u32
+DOMAIN_DEPOSIT = 3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=1 << 16, help="verifies per rank per step")
+    ap.add_argument("--committees", type=int, default=1024)
+    ap.add_argument("--committee-size", type=int, default=128)
+    ap.add_argument("--cpu-sample", type=int, default=256)
+    ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-aggregate", action="store_true")
+    return ap.parse_args()
+
+
+def make_workload(native, n, seed):
+    """2^16 signed deposit items built on the GPU (untimed), 1/16 tampered."""
+    rng = np.random.default_rng(seed)
+    r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    sks = bytearray()
+    for _ in range(n):
+        k = int.from_bytes(rng.bytes(32), "big") % (r - 1) + 1
+        sks += k.to_bytes(32, "big")
+    sks = bytes(sks)
+    msgs = bytearray(rng.bytes(32 * n))
+    doms = DOMAIN_DEPOSIT.to_bytes(8, "big") * n
+    pks = native.privtopub_batch(sks)
+    sigs = bytearray(native.sign_batch(bytes(msgs), sks, doms))
+    expected = np.ones(n, dtype=bool)
+    for i in range(3, n, 16):              # 1/16 tampered, full verification work
+        if (i // 16) % 2 == 0:
+            msgs[32 * i] ^= 0x01           # message bit flip
+        else:
+            j = (i + 1) % n
+            sigs[96 * i:96 * i + 96] = sigs[96 * j:96 * j + 96]   # signature of another item
+        expected[i] = False
+    return pks, bytes(msgs), bytes(sigs), doms, expected
+
+
+def load_valu_peak():
+    try:
+        with open(VALU_PEAK_FILE) as f:
+            d = json.load(f)
+        return float(d["v_mad_u64_u32_Tops"]), VALU_PEAK_FILE
+    except Exception:
+        return None, None
+
+
+def count_fp_muls(pks, msgs, sigs, doms, k=8):
+    """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build."""
+    import build_native
+    path = build_native.build_hostcheck(count_ops=True)
+    L = ctypes.CDLL(path)
+    tot = np.zeros(5)
+    done = 0
+    for i in range(64):
+        out = (ctypes.c_uint64 * 5)()
+        if L.hc_count_verify_stages(pks[48 * i:48 * i + 48], msgs[32 * i:32 * i + 32],
+                                    sigs[96 * i:96 * i + 96], doms[8 * i:8 * i + 8], out) == 1:
+            tot += np.array(list(out), dtype=float)
+            done += 1
+            if done == k:
+                break
+    names = ["decode_g1", "decode_g2", "hash_to_g2", "miller_loop_2", "final_exp"]
+    return {nm: tot[j] / done for j, nm in enumerate(names)}
+
+
+def _cpu_verify(args):
+    import bls_oracle as O
+    pk, m, s, d = args
+    return O.verify(m, pk, s, d)
+
+
+def cpu_baseline(pks, msgs, sigs, sample, procs):
+    """Oracle (py_ecc 1.7.0 algorithm restatement) verify on host cores, bounded sample."""
+    import multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    items = [(pks[48 * i:48 * i + 48], msgs[32 * i:32 * i + 32], sigs[96 * i:96 * i + 96], DOMAIN_DEPOSIT)
+             for i in range(sample)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_verify, items, chunksize=1)
+    dt = time.perf_counter() - t0
+    return sample / dt, res, dt
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    from bls381_amd import _native as native
+    native.init(local_rank)
+    L = native.lib()
+
+    # ---------------- workload, device-resident
+    n = args.n
+    pks, msgs, sigs, doms, expected = make_workload(native, n, 0xB15_0001 + rank)
+    dev = torch.device("cuda", local_rank)
+    t_u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_pks, d_msgs, d_sigs, d_doms = t_u8(pks), t_u8(msgs), t_u8(sigs), t_u8(doms)
+    d_ver = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.bls381_verify_batch_workspace_size(n), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        rc = L.bls381_verify_batch_device(n, d_pks.data_ptr(), d_msgs.data_ptr(), d_sigs.data_ptr(),
+                                          d_doms.data_ptr(), d_ver.data_ptr(), ws.data_ptr(),
+                                          ctypes.c_void_p(stream.cuda_stream))
+        native.check(rc)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    native.profile_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    prof = native.profile_read()
+    native.profile_enable(False)
+    got = d_ver.cpu().numpy().astype(bool)
+    if not np.array_equal(got, expected):
+        raise SystemExit("verdict mismatch on rank %d: %d wrong" % (rank, int((got != expected).sum())))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_items = n * args.steps * world
+    value = total_items / elapsed
+
+    # ---------------- committee aggregation (C3 shape), device-resident
+    agg = None
+    if not args.no_aggregate:
+        nc, cs = args.committees, args.committee_size
+        # distinct committees drawn from the 2^16 generated keys (131072 member slots)
+        rng = np.random.default_rng(0xB15_0003 + rank)
+        idx = rng.integers(0, n, nc * cs)
+        pk_arr = np.frombuffer(pks, dtype=np.uint8).reshape(n, 48)
+        cpks = pk_arr[idx].tobytes()
+        offsets = np.arange(0, nc * cs + 1, cs, dtype=np.uint32)
+        d_cpks = t_u8(cpks)
+        d_out = torch.zeros(nc * 48, dtype=torch.uint8, device=dev)
+        d_st = torch.zeros(nc, dtype=torch.int32, device=dev)
+        aws = torch.empty(L.bls381_aggregate_pubkeys_batch_workspace_size(nc, nc * cs), dtype=torch.uint8, device=dev)
+
+        def astep():
+            native.check(L.bls381_aggregate_pubkeys_batch_device(
+                nc, offsets.ctypes.data_as(ctypes.c_void_p), nc * cs, d_cpks.data_ptr(), d_out.data_ptr(),
+                d_st.data_ptr(), aws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        astep()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        a_steps = max(args.steps, 3)
+        t0 = time.perf_counter()
+        for _ in range(a_steps):
+            astep()
+        torch.cuda.synchronize()
+        at = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([at], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            at = float(t.item())
+        assert int(d_st.abs().sum().item()) == 0
+        agg = {"workload": "C3: %d committees x %d pubkeys, bls_aggregate_pubkeys each" % (nc, cs),
+               "committee_aggregations_per_s": nc * a_steps * world / at,
+               "pubkeys_aggregated_per_s": nc * cs * a_steps * world / at,
+               "ms_per_step": 1e3 * at / a_steps}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    # ---------------- roofline of the dominant kernel (live HIP-event times)
+    counts = count_fp_muls(pks, msgs, sigs, doms)
+    kern_ms = {k: v["total_ms"] / v["count"] for k, v in prof.items()}
+    dom_k = max(kern_ms, key=kern_ms.get)
+    peak, peak_src = load_valu_peak()
+    launch_macs = counts.get(dom_k, 0.0) * MACS_PER_FP_MUL * n
+    achieved = launch_macs / (kern_ms[dom_k] * 1e-3) / 1e12
+    roofline = {"bound": "valu-int32", "kernel": dom_k, "achieved": round(achieved, 3),
+                "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
+                "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
+                "macs_per_launch": launch_macs,
+                "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
+                "peak_source": peak_src}
+    whole = sum(counts.values()) * MACS_PER_FP_MUL * n / (1e-3 * sum(kern_ms.values())) / 1e12
+    roofline["pipeline_achieved"] = round(whole, 3)
+    roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        rate, res, dt = cpu_baseline(pks, msgs, sigs, args.cpu_sample, args.cpu_procs)
+        assert list(res) == list(expected[:args.cpu_sample]), "CPU oracle disagrees with GPU verdicts"
+        cpu = {"value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
+               "sample": "first %d items of the same C2 batch, oracle/bls_oracle.py verify (py_ecc 1.7.0 "
+                         "algorithm restatement: Fq12-coordinate Miller loop, naive final exponentiation), "
+                         "multiprocessing.Pool(%d), %.1f s wall" % (args.cpu_sample, args.cpu_procs, dt)}
+
+    line = {
+        "metric": "BLS sig verifications/sec (whole node)",
+        "value": round(value, 2),
+        "unit": "verifications/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)",
+        "data": "synthetic (random keys/messages, signatures made on device)",
+        "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
+                   "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "aggregation": agg,
+    }
+    print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,136 @@
+"""Drop-in replacement for the reference's `eth2spec.utils.bls`
+(test_libs/pyspec/eth2spec/utils/bls.py:1-46), backed by the gfx950 engine.
+
+Same module attributes (`bls_active`, `STUB_SIGNATURE`, `STUB_PUBKEY`,
+`only_with_bls`), same function names and keyword names, same return types and
+the same error behaviour as the py_ecc 1.7.0 calls they replace
+(SURVEY.md Appendix A):
+
+* bls_verify / bls_verify_multiple return False for undecodable or invalid
+  inputs (py_ecc catches ValidationError/ValueError/AssertionError);
+* bls_verify_multiple raises ValidationError (a ValueError) on a length mismatch;
+* bls_aggregate_* raise ValueError on an invalid point encoding;
+* a domain outside [0, 2^64) raises OverflowError (int.to_bytes).
+"""
+from . import _native
+
+# Flag to make BLS active or not (bls.py:3-4).  Tests flip it through the
+# module attribute (eth2spec/test/context.py:79-90).
+bls_active = True
+
+STUB_SIGNATURE = b'\x11' * 96
+STUB_PUBKEY = b'\x22' * 48
+
+# py_ecc 1.7.0 serialises the int domain big-endian; one switch.
+DOMAIN_BYTEORDER = "big"
+
+
+class ValidationError(ValueError):
+    """Mirror of eth_utils.ValidationError raised by py_ecc.verify_multiple."""
+
+
+def only_with_bls(alt_return=None):
+    """
+    Decorator factory to make a function only run when BLS is active. Otherwise return the default.
+    (bls.py:10-21; the flag is read at call time from this module.)
+    """
+    def runner(fn):
+        def entry(*args, **kw):
+            if bls_active:
+                return fn(*args, **kw)
+            else:
+                return alt_return
+        return entry
+    return runner
+
+
+def _dom8(domain) -> bytes:
+    return int(domain).to_bytes(8, DOMAIN_BYTEORDER)
+
+
+def _sk32(privkey) -> bytes:
+    k = int(privkey)
+    if k < 0:
+        raise ValueError("negative private key")
+    # [k]P == [k mod r]P on the prime-order groups; py_ecc multiplies by k itself
+    r = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
+    if k >= 1 << 256:
+        k %= r
+    return k.to_bytes(32, "big")
+
+
+@only_with_bls(alt_return=True)
+def bls_verify(pubkey, message_hash, signature, domain):
+    dom8 = _dom8(domain)
+    pubkey, message_hash, signature = bytes(pubkey), bytes(message_hash), bytes(signature)
+    if len(pubkey) != 48 or len(signature) != 96 or len(message_hash) > _native.MSG_MAX:
+        return False
+    return _native.verify(pubkey, message_hash, signature, dom8)
+
+
+@only_with_bls(alt_return=True)
+def bls_verify_multiple(pubkeys, message_hashes, signature, domain):
+    if len(pubkeys) != len(message_hashes):
+        raise ValidationError(
+            "len(pubkeys) (%s) should be equal to len(message_hashes) (%s)" % (len(pubkeys), len(message_hashes)))
+    dom8 = _dom8(domain)
+    pks = [bytes(p) for p in pubkeys]
+    msgs = [bytes(m) for m in message_hashes]
+    signature = bytes(signature)
+    if any(len(p) != 48 for p in pks) or len(signature) != 96:
+        return False
+    lens = {len(m) for m in msgs}
+    if len(lens) > 1 or (lens and max(lens) > _native.MSG_MAX):
+        return False  # mixed-length messages are outside the engine's batch layout
+    mlen = lens.pop() if lens else 32
+    return _native.verify_multiple(b"".join(pks), b"".join(msgs), mlen, signature, dom8)
+
+
+@only_with_bls(alt_return=STUB_PUBKEY)
+def bls_aggregate_pubkeys(pubkeys):
+    pks = [bytes(p) for p in pubkeys]
+    if any(len(p) != 48 for p in pks):
+        raise ValueError("pubkeys must be 48 bytes")
+    return _native.aggregate_pubkeys(b"".join(pks))
+
+
+@only_with_bls(alt_return=STUB_SIGNATURE)
+def bls_aggregate_signatures(signatures):
+    sigs = [bytes(s) for s in signatures]
+    if any(len(s) != 96 for s in sigs):
+        raise ValueError("signatures must be 96 bytes")
+    return _native.aggregate_signatures(b"".join(sigs))
+
+
+@only_with_bls(alt_return=STUB_SIGNATURE)
+def bls_sign(message_hash, privkey, domain):
+    message_hash = bytes(message_hash)
+    if len(message_hash) > _native.MSG_MAX:
+        raise ValueError("message longer than the engine's limit")
+    return _native.sign(message_hash, _sk32(privkey), _dom8(domain))
+
+
+# ---- py_ecc.bls extras used by the reference's helpers / vector generator
+def privtopub(privkey) -> bytes:
+    """py_ecc bls.privtopub (eth2spec/test/helpers/keys.py:5, test_generators/bls/main.py:114)."""
+    return _native.privtopub(_sk32(privkey))
+
+
+def hash_to_G2_compressed(message_hash, domain) -> bytes:
+    """compress_G2(hash_to_G2(m, d)) as 96 bytes (test_generators/bls/main.py:84-85)."""
+    comp, _ = _native.hash_to_g2(bytes(message_hash), _dom8(domain))
+    return comp
+
+
+def hash_to_G2_affine(message_hash, domain):
+    """Normalised affine ((x_re, x_im), (y_re, y_im)) as ints."""
+    _, aff = _native.hash_to_g2(bytes(message_hash), _dom8(domain))
+    v = [int.from_bytes(aff[48 * k:48 * k + 48], "big") for k in range(4)]
+    return (v[0], v[1]), (v[2], v[3])
+
+
+def hash_to_G2_pyecc_projective(message_hash, domain):
+    """py_ecc's un-normalised projective triple (test_generators/bls/main.py:66-72)."""
+    out = _native.hash_to_g2_pyecc_projective(bytes(message_hash), _dom8(domain))
+    v = [int.from_bytes(out[48 * k:48 * k + 48], "big") for k in range(6)]
+    return ((v[0], v[1]), (v[2], v[3]), (v[4], v[5]))

@@ -1,0 +1,78 @@
+"""Build the native libraries in-tree (lib/*.so travel to the GPU box with the snapshot).
+
+* lib/libbls381.so            -- the product: hipcc --offload-arch=gfx950, C ABI of include/bls381.h
+* lib/libbls381_hostcheck.so  -- test infrastructure: g++ build of the same arithmetic headers
+* tools/valu_peak             -- integer-VALU peak microbenchmark (roofline denominator)
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+INC = os.path.join(ROOT, "include")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+HIP_SOURCES = ["bls381_capi.hip"]
+HEADERS = ["bls381_defs.hpp", "bls381_consts.hpp", "bls381_field.hpp", "bls381_curve.hpp", "bls381_hash.hpp",
+           "bls381_pairing.hpp", "bls381_kernels.hpp"]
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return False
+    t = os.path.getmtime(target)
+    return all(os.path.getmtime(d) <= t for d in deps)
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build_hip(force=False, extra=()):
+    os.makedirs(LIB, exist_ok=True)
+    out = os.path.join(LIB, "libbls381.so")
+    deps = [os.path.join(CSRC, f) for f in HIP_SOURCES + HEADERS] + [os.path.join(INC, "bls381.h")]
+    if not force and _newer(out, deps):
+        return out
+    _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INC, "-I", CSRC,
+          *extra, *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", out])
+    return out
+
+
+def build_hostcheck(force=False, sanitize=False, count_ops=False):
+    os.makedirs(LIB, exist_ok=True)
+    name = "libbls381_hostcheck_asan.so" if sanitize else (
+        "libbls381_hostcheck_count.so" if count_ops else "libbls381_hostcheck.so")
+    out = os.path.join(LIB, name)
+    src = os.path.join(CSRC, "host_check.cpp")
+    deps = [src] + [os.path.join(CSRC, f) for f in HEADERS if f != "bls381_kernels.hpp"]
+    if not force and _newer(out, deps):
+        return out
+    cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-I", CSRC, src, "-o", out]
+    if sanitize:
+        cmd[3:3] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+    if count_ops:
+        cmd[3:3] = ["-DBLS_COUNT_OPS"]
+    _run(cmd)
+    return out
+
+
+def build_valu_peak(force=False):
+    src = os.path.join(ROOT, "tools", "valu_peak.hip")
+    out = os.path.join(ROOT, "tools", "valu_peak")
+    if not force and _newer(out, [src]):
+        return out
+    _run([HIPCC, "--offload-arch=gfx950", "-O3", src, "-o", out])
+    return out
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    build_hostcheck(force)
+    build_hostcheck(force, count_ops=True)
+    build_valu_peak(force)
+    build_hip(force)

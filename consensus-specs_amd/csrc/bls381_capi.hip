@@ -1,0 +1,840 @@
+// C ABI of the MI355X BLS12-381 engine (include/bls381.h).
+//
+// Host runtime: one context per device (stream + grow-only workspace), the
+// launch pipelines for each entry point, HIP-event kernel accounting for
+// bench.py.  No CPU fallback: without a gfx950 device every entry point
+// returns BLS381_ENODEV.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "bls381.h"
+#include "bls381_kernels.hpp"
+
+using namespace bls381;
+
+namespace {
+
+thread_local std::string t_err;
+thread_local int t_device = -1;
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  void* ws = nullptr;
+  size_t ws_cap = 0;
+  std::mutex mu;
+};
+
+std::mutex g_mu;
+std::vector<Ctx*> g_ctx;
+
+// ---- profiling: per-kernel HIP events on the launch stream
+struct ProfEv { const char* name; hipEvent_t a, b; };
+std::mutex g_prof_mu;
+bool g_prof_on = false;
+std::vector<ProfEv> g_prof_pending;
+std::map<std::string, std::pair<long, double>> g_prof_acc;
+
+int fail(const char* what, hipError_t e) {
+  t_err = std::string(what) + ": " + hipGetErrorString(e);
+  return BLS381_EHIP;
+}
+
+#define HIPC(x)                                   \
+  do {                                            \
+    hipError_t e__ = (x);                         \
+    if (e__ != hipSuccess) return fail(#x, e__);  \
+  } while (0)
+
+Ctx* get_ctx(int* rc) {
+  int dev = t_device;
+  if (dev < 0) {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) {
+      t_err = "no HIP device";
+      *rc = BLS381_ENODEV;
+      return nullptr;
+    }
+    dev = 0;
+    t_device = 0;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  if ((int)g_ctx.size() <= dev) g_ctx.resize(dev + 1, nullptr);
+  if (!g_ctx[dev]) {
+    if (hipSetDevice(dev) != hipSuccess) { t_err = "hipSetDevice failed"; *rc = BLS381_ENODEV; return nullptr; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+        std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      t_err = std::string("device is not gfx950: ") + prop.gcnArchName;
+      *rc = BLS381_ENODEV;
+      return nullptr;
+    }
+    Ctx* c = new Ctx();
+    c->device = dev;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
+    }
+    g_ctx[dev] = c;
+  }
+  if (hipSetDevice(dev) != hipSuccess) { t_err = "hipSetDevice failed"; *rc = BLS381_ENODEV; return nullptr; }
+  *rc = 0;
+  return g_ctx[dev];
+}
+
+int ensure_ws(Ctx* c, size_t bytes) {
+  if (c->ws_cap >= bytes) return 0;
+  if (c->ws) { HIPC(hipStreamSynchronize(c->stream)); HIPC(hipFree(c->ws)); c->ws = nullptr; c->ws_cap = 0; }
+  size_t cap = bytes + bytes / 4 + (1 << 20);
+  HIPC(hipMalloc(&c->ws, cap));
+  c->ws_cap = cap;
+  return 0;
+}
+
+// bump allocator over a workspace, 256-byte aligned slices
+struct Bump {
+  uint8_t* base;
+  size_t off = 0;
+  explicit Bump(void* b) : base((uint8_t*)b) {}
+  template <class T> T* take(size_t count) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = (T*)(base + off);
+    off += count * sizeof(T);
+    return p;
+  }
+};
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+unsigned grid_for(size_t n, int block = KBLOCK) { return (unsigned)((n + block - 1) / block); }
+
+template <class K, class... A>
+int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... args) {
+  if (grid.x == 0) return 0;
+  ProfEv ev{name, nullptr, nullptr};
+  const bool prof = g_prof_on;
+  if (prof) {
+    HIPC(hipEventCreate(&ev.a));
+    HIPC(hipEventCreate(&ev.b));
+    HIPC(hipEventRecord(ev.a, s));
+  }
+  hipLaunchKernelGGL(kern, grid, block, 0, s, args...);
+  HIPC(hipGetLastError());
+  if (prof) {
+    HIPC(hipEventRecord(ev.b, s));
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    g_prof_pending.push_back(ev);
+  }
+  return 0;
+}
+
+#define LAUNCH(name, s, grid, block, kern, ...)                     \
+  do {                                                              \
+    int rc__ = launch(name, s, grid, block, kern, __VA_ARGS__);     \
+    if (rc__) return rc__;                                          \
+  } while (0)
+
+// ----------------------------------------------------- verify_batch (C2) --
+struct VerifyWs {
+  uint32_t *pk_aff, *sig_aff, *h_aff, *f;
+  uint8_t *pk_st, *sig_st, *f_st;
+};
+size_t verify_ws_size(size_t n) {
+  return align256(24 * 4 * n) + align256(48 * 4 * n) * 2 + align256(144 * 4 * n) + 3 * align256(n) + 1024;
+}
+VerifyWs carve_verify(void* ws, size_t n) {
+  Bump b(ws);
+  VerifyWs w;
+  w.pk_aff = b.take<uint32_t>(24 * n);
+  w.sig_aff = b.take<uint32_t>(48 * n);
+  w.h_aff = b.take<uint32_t>(48 * n);
+  w.f = b.take<uint32_t>(144 * n);
+  w.pk_st = b.take<uint8_t>(n);
+  w.sig_st = b.take<uint8_t>(n);
+  w.f_st = b.take<uint8_t>(n);
+  return w;
+}
+
+int run_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* doms,
+                     uint8_t* verdicts, void* ws, hipStream_t s) {
+  VerifyWs w = carve_verify(ws, n);
+  const dim3 g(grid_for(n)), b(KBLOCK);
+  LAUNCH("decode_g1", s, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
+  LAUNCH("decode_g2", s, g, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
+  LAUNCH("hash_to_g2", s, g, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  LAUNCH("miller_loop_2", s, g, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
+         (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
+  LAUNCH("final_exp", s, g, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
+  return 0;
+}
+
+// --------------------------------------------------------- aggregation --
+// plan chunk levels for groups given by host offsets
+struct AggPlan {
+  std::vector<std::vector<agg_chunk>> levels;   // chunks per level
+};
+constexpr uint32_t CHUNK_L1 = 4 * KBLOCK;
+constexpr uint32_t CHUNK_LN = 4 * KBLOCK;
+
+AggPlan plan_agg(size_t ng, const uint32_t* offsets) {
+  AggPlan p;
+  std::vector<uint32_t> cur_off(offsets, offsets + ng + 1);
+  uint32_t chunk = CHUNK_L1;
+  bool first = true;
+  while (true) {
+    std::vector<agg_chunk> lv;
+    std::vector<uint32_t> next_off(ng + 1, 0);
+    bool multi = false;
+    for (size_t g = 0; g < ng; ++g) {
+      next_off[g] = (uint32_t)lv.size();
+      const uint32_t b0 = cur_off[g], e0 = cur_off[g + 1];
+      if (e0 <= b0) { lv.push_back({b0, b0}); continue; }
+      uint32_t cnt = 0;
+      for (uint32_t x = b0; x < e0; x += chunk) { lv.push_back({x, x + chunk < e0 ? x + chunk : e0}); ++cnt; }
+      if (cnt > 1) multi = true;
+    }
+    next_off[ng] = (uint32_t)lv.size();
+    p.levels.push_back(lv);
+    if (!multi && !first) break;
+    if (!multi) break;
+    cur_off = next_off;
+    chunk = CHUNK_LN;
+    first = false;
+  }
+  return p;
+}
+
+size_t agg_ws_size(const AggPlan& p, int ncomp) {
+  size_t s = 1024;
+  for (auto& lv : p.levels) s += align256(lv.size() * sizeof(agg_chunk)) + align256(lv.size() * ncomp * 48) + align256(lv.size());
+  return s;
+}
+
+// runs the plan; returns device pointers to the final per-group Jacobian sums / bad flags
+template <class F>
+int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStream_t s,
+            const uint32_t** out_jac, const uint8_t** out_bad, size_t* used) {
+  Bump b(ws);
+  const uint32_t* prev_jac = nullptr;
+  const uint8_t* prev_bad = nullptr;
+  size_t prev_n = 0;
+  for (size_t l = 0; l < p.levels.size(); ++l) {
+    const auto& lv = p.levels[l];
+    agg_chunk* d_chunks = b.take<agg_chunk>(lv.size());
+    uint32_t* jac = b.take<uint32_t>(lv.size() * soa_jac<F>::NC * 12);
+    uint8_t* bad = b.take<uint8_t>(lv.size());
+    HIPC(hipMemcpyAsync(d_chunks, lv.data(), lv.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+    if (l == 0) {
+      LAUNCH("agg_decode_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, true>), (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0, (const uint8_t*)nullptr, jac, bad);
+    } else {
+      LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, false>), (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad);
+    }
+    prev_jac = jac;
+    prev_bad = bad;
+    prev_n = lv.size();
+  }
+  (void)ng;
+  *out_jac = prev_jac;
+  *out_bad = prev_bad;
+  *used = b.off;
+  return 0;
+}
+
+// ------------------------------------------------- verify_multiple pieces --
+// Groups pks by distinct message (first-appearance order), as py_ecc's
+// verify_multiple does.
+struct VmHost {
+  std::vector<uint8_t> pks_perm;     // pks reordered by group
+  std::vector<uint32_t> offsets;     // group offsets into pks_perm
+  std::vector<uint8_t> msgs;         // distinct messages, msg_len each
+};
+VmHost group_by_message(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t mlen) {
+  VmHost h;
+  std::unordered_map<std::string, uint32_t> idx;
+  std::vector<std::vector<uint32_t>> members;
+  for (size_t i = 0; i < n; ++i) {
+    std::string key((const char*)msgs + mlen * i, mlen);
+    auto it = idx.find(key);
+    uint32_t g;
+    if (it == idx.end()) {
+      g = (uint32_t)members.size();
+      idx.emplace(key, g);
+      members.emplace_back();
+      h.msgs.insert(h.msgs.end(), msgs + mlen * i, msgs + mlen * (i + 1));
+    } else {
+      g = it->second;
+    }
+    members[g].push_back((uint32_t)i);
+  }
+  h.offsets.push_back(0);
+  for (auto& m : members) {
+    for (uint32_t i : m) h.pks_perm.insert(h.pks_perm.end(), pks + 48 * i, pks + 48 * (i + 1));
+    h.offsets.push_back((uint32_t)(h.pks_perm.size() / 48));
+  }
+  return h;
+}
+
+// pair k < G: (H(msg_k), agg_k); pair G (if with_sig): (sig, -g1).  Statuses:
+// any BAD -> BAD; an infinite operand contributes 1.
+__global__ void __launch_bounds__(KBLOCK) k_miller_vm(size_t G, int with_sig, const uint32_t* __restrict__ h_aff,
+                                                     const uint8_t* __restrict__ h_st,
+                                                     const uint32_t* __restrict__ agg_aff,
+                                                     const uint8_t* __restrict__ agg_st,
+                                                     const uint32_t* __restrict__ sig_aff,
+                                                     const uint8_t* __restrict__ sig_st,
+                                                     uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t np = G + (with_sig ? 1 : 0);
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= np) return;
+  uint8_t sq, sp;
+  aff_t<fp2_t> Q;
+  aff_t<fp_t> P;
+  if (k < G) {
+    sq = h_st[k];
+    sp = agg_st[k];
+    if (sq == ST_OK && sp == ST_OK) { Q = soa_ld_g2(h_aff, G, k); P = soa_ld_g1(agg_aff, G, k); }
+  } else {
+    sq = sig_st[0];
+    sp = ST_OK;
+    if (sq == ST_OK) { Q = soa_ld_g2(sig_aff, 1, 0); P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M; }
+  }
+  fp12_t f = fp12_one();
+  uint8_t st = ST_OK;
+  if (sq == ST_BAD || sp == ST_BAD) st = ST_BAD;
+  else if (sq == ST_OK && sp == ST_OK) f = miller_loop_1(Q, g1_prepare(P));
+  soa_st12(f_out, np, k, f);
+  st_out[k] = st;
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_fp12_pair_product_st(size_t m, const uint32_t* __restrict__ in,
+                                                                const uint8_t* __restrict__ in_st,
+                                                                uint32_t* __restrict__ out, uint8_t* __restrict__ out_st) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t half = (m + 1) / 2;
+  if (j >= half) return;
+  fp12_t a = soa_ld12(in, m, 2 * j);
+  uint8_t st = in_st[2 * j];
+  if (2 * j + 1 < m) {
+    a = fp12_mul(a, soa_ld12(in, m, 2 * j + 1));
+    if (in_st[2 * j + 1] != ST_OK) st = ST_BAD;
+  }
+  soa_st12(out, half, j, a);
+  out_st[j] = st;
+}
+
+// reduce m Fp12 (+status) to one by pairwise product passes; returns final buffers
+int reduce_fp12(size_t m, uint32_t* f, uint8_t* st, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st) {
+  while (m > 1) {
+    const size_t half = (m + 1) / 2;
+    uint32_t* nf = b.take<uint32_t>(144 * half);
+    uint8_t* nst = b.take<uint8_t>(half);
+    LAUNCH("fp12_product", s, dim3(grid_for(half)), dim3(KBLOCK), k_fp12_pair_product_st, m, (const uint32_t*)f,
+           (const uint8_t*)st, nf, nst);
+    f = nf;
+    st = nst;
+    m = half;
+  }
+  *out_f = f;
+  *out_st = st;
+  return 0;
+}
+
+// Everything of a verify_multiple call up to (and excluding) the final
+// exponentiation.  Leaves the single Fp12 product and its status on device.
+int vm_partial(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, size_t mlen, const uint8_t* sig,
+               int with_sig, const uint8_t* dom8, uint32_t** d_f, uint8_t** d_st, Bump& b) {
+  hipStream_t s = c->stream;
+  VmHost h = group_by_message(n, pks, msgs, mlen);
+  const size_t G = h.offsets.size() - 1;
+  AggPlan plan = plan_agg(G, h.offsets.data());
+  // inputs
+  uint8_t* d_pks = b.take<uint8_t>(h.pks_perm.size() + 1);
+  uint8_t* d_msgs = b.take<uint8_t>(h.msgs.size() + 1);
+  uint8_t* d_sig = b.take<uint8_t>(96);
+  uint8_t* d_dom = b.take<uint8_t>(8);
+  if (!h.pks_perm.empty()) HIPC(hipMemcpyAsync(d_pks, h.pks_perm.data(), h.pks_perm.size(), hipMemcpyHostToDevice, s));
+  if (!h.msgs.empty()) HIPC(hipMemcpyAsync(d_msgs, h.msgs.data(), h.msgs.size(), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sig, sig, 96, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_dom, dom8, 8, hipMemcpyHostToDevice, s));
+  // group sums -> affine + subgroup check
+  uint32_t* agg_aff = b.take<uint32_t>(24 * (G + 1));
+  uint8_t* agg_st = b.take<uint8_t>(G + 1);
+  if (G > 0) {
+    const uint32_t* jac;
+    const uint8_t* bad;
+    size_t used = 0;
+    uint8_t* sub = b.take<uint8_t>(0);
+    int rc = run_agg<fp_t>(plan, G, d_pks, sub, s, &jac, &bad, &used);
+    if (rc) return rc;
+    b.off += used;
+    LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
+  }
+  // hashes of distinct messages
+  uint32_t* h_aff = b.take<uint32_t>(48 * (G + 1));
+  uint8_t* h_st = b.take<uint8_t>(G + 1);
+  if (G > 0)
+    LAUNCH("hash_to_g2", s, dim3(grid_for(G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
+           (const uint8_t*)d_dom, 0, h_aff, h_st);
+  // signature
+  uint32_t* sig_aff = b.take<uint32_t>(48);
+  uint8_t* sig_st = b.take<uint8_t>(1);
+  LAUNCH("decode_g2", s, dim3(1), dim3(KBLOCK), k_decode_g2, (size_t)1, (const uint8_t*)d_sig, sig_aff, sig_st, 1);
+  const size_t np = G + (with_sig ? 1 : 0);
+  if (np == 0) {
+    // empty product: f = 1 (py_ecc's FQ12.one() start value)
+    uint32_t* f = b.take<uint32_t>(144);
+    uint8_t* st = b.take<uint8_t>(1);
+    std::vector<uint8_t> one(576, 0);
+    one[47] = 1;
+    uint8_t* tmp = b.take<uint8_t>(576);
+    HIPC(hipMemcpyAsync(tmp, one.data(), 576, hipMemcpyHostToDevice, s));
+    LAUNCH("fp12_from_bytes", s, dim3(1), dim3(KBLOCK), k_fp12_from_bytes, (size_t)1, (const uint8_t*)tmp, f);
+    HIPC(hipMemsetAsync(st, 0, 1, s));
+    // the host vector must outlive the async copy
+    HIPC(hipStreamSynchronize(s));
+    *d_f = f;
+    *d_st = st;
+    return 0;
+  }
+  uint32_t* f = b.take<uint32_t>(144 * np);
+  uint8_t* st = b.take<uint8_t>(np);
+  LAUNCH("miller_loop_1", s, dim3(grid_for(np)), dim3(KBLOCK), k_miller_vm, G, with_sig, (const uint32_t*)h_aff,
+         (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, (const uint32_t*)sig_aff,
+         (const uint8_t*)sig_st, f, st);
+  return reduce_fp12(np, f, st, b, s, d_f, d_st);
+}
+
+size_t vm_ws_bound(size_t n, size_t mlen) {
+  // generous bound: inputs + per-group buffers + agg levels + Miller tree
+  const size_t G = n + 1;
+  return 4096 + align256(48 * n) + align256(mlen * n) + 2 * 1024 +
+         align256(24 * 4 * G) + align256(G) + align256(48 * 4 * G) + align256(G) + 1024 +
+         3 * (align256(144 * 4 * G) + align256(G)) + 2 * (align256(G * 12) + align256(G * 36 * 4) + align256(G)) +
+         (size_t)(2 * G / (CHUNK_L1) + 64) * (36 * 4 + 16);
+}
+
+}  // namespace
+
+// ====================================================================== ABI
+extern "C" {
+
+int bls381_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+int bls381_init(int device) {
+  int cnt = bls381_device_count();
+  if (cnt <= 0) { t_err = "no HIP device"; return BLS381_ENODEV; }
+  if (device < 0 || device >= cnt) { t_err = "device ordinal out of range"; return BLS381_EARG; }
+  t_device = device;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  return c ? 0 : rc;
+}
+
+void bls381_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (Ctx* c : g_ctx) {
+    if (!c) continue;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->ws) (void)hipFree(c->ws);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+  }
+  g_ctx.clear();
+}
+
+const char* bls381_last_error(void) { return t_err.c_str(); }
+
+int bls381_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_prof_on = on != 0;
+  g_prof_acc.clear();
+  for (auto& e : g_prof_pending) { (void)hipEventDestroy(e.a); (void)hipEventDestroy(e.b); }
+  g_prof_pending.clear();
+  return 0;
+}
+
+int bls381_profile_read(char* out, size_t cap) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& e : g_prof_pending) {
+    float ms = 0;
+    if (hipEventSynchronize(e.b) != hipSuccess) return BLS381_EHIP;
+    if (hipEventElapsedTime(&ms, e.a, e.b) != hipSuccess) return BLS381_EHIP;
+    auto& acc = g_prof_acc[e.name];
+    acc.first += 1;
+    acc.second += ms;
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  g_prof_pending.clear();
+  std::string js = "{";
+  bool first = true;
+  for (auto& kv : g_prof_acc) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), "%s\"%s\": {\"count\": %ld, \"total_ms\": %.6f}", first ? "" : ", ",
+                  kv.first.c_str(), kv.second.first, kv.second.second);
+    js += buf;
+    first = false;
+  }
+  js += "}";
+  if (js.size() + 1 > cap) return BLS381_EARG;
+  std::memcpy(out, js.c_str(), js.size() + 1);
+  return (int)js.size();
+}
+
+size_t bls381_verify_batch_workspace_size(size_t n) { return verify_ws_size(n); }
+
+int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32, const uint8_t* d_sigs,
+                               const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace, void* stream) {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n == 0) return 0;
+  if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace) return BLS381_EARG;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return run_verify_batch(n, d_pks, d_msgs32, d_sigs, d_dom8s, d_verdicts, d_workspace, s);
+}
+
+int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
+                        const uint8_t* dom8s, uint8_t* verdicts_out) {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n == 0) return 0;
+  if (!pks || !msgs32 || !sigs || !dom8s || !verdicts_out) return BLS381_EARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t in_bytes = align256(48 * n) + align256(32 * n) + align256(96 * n) + align256(8 * n) + align256(n);
+  if ((rc = ensure_ws(c, in_bytes + verify_ws_size(n) + 1024))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_pks = b.take<uint8_t>(48 * n);
+  uint8_t* d_msgs = b.take<uint8_t>(32 * n);
+  uint8_t* d_sigs = b.take<uint8_t>(96 * n);
+  uint8_t* d_doms = b.take<uint8_t>(8 * n);
+  uint8_t* d_v = b.take<uint8_t>(n);
+  void* ws = b.take<uint8_t>(verify_ws_size(n));
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_pks, pks, 48 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_msgs, msgs32, 32 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n, hipMemcpyHostToDevice, s));
+  if ((rc = run_verify_batch(n, d_pks, d_msgs, d_sigs, d_doms, d_v, ws, s))) return rc;
+  HIPC(hipMemcpyAsync(verdicts_out, d_v, n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_verify(const uint8_t pk[48], const uint8_t* msg, size_t msg_len, const uint8_t sig[96],
+                  const uint8_t dom8[8]) {
+  if (!pk || !sig || !dom8 || (!msg && msg_len)) return BLS381_EARG;
+  if (msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  if (msg_len == 32) {
+    uint8_t v = 0;
+    int rc = bls381_verify_batch(1, pk, msg, sig, dom8, &v);
+    return rc ? rc : v;
+  }
+  // general message length: one-pair-per-lane path of verify_multiple
+  return bls381_verify_multiple(1, pk, msg, msg_len, sig, dom8);
+}
+
+int bls381_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len, const uint8_t sig[96],
+                           const uint8_t dom8[8]) {
+  if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, vm_ws_bound(n, msg_len)))) return rc;
+  Bump b(c->ws);
+  uint32_t* f;
+  uint8_t* st;
+  if ((rc = vm_partial(c, n, pks, msgs, msg_len, sig, 1, dom8, &f, &st, b))) return rc;
+  uint8_t* d_v = b.take<uint8_t>(1);
+  LAUNCH("final_exp", c->stream, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)f,
+         (const uint8_t*)st, d_v);
+  uint8_t v = 0;
+  HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return v;
+}
+
+int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len, const uint8_t sig[96],
+                          int include_sig, const uint8_t dom8[8], uint8_t out576[576]) {
+  if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || !out576 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, vm_ws_bound(n, msg_len)))) return rc;
+  Bump b(c->ws);
+  uint32_t* f;
+  uint8_t* st;
+  if ((rc = vm_partial(c, n, pks, msgs, msg_len, sig, include_sig ? 1 : 0, dom8, &f, &st, b))) return rc;
+  uint8_t* d_out = b.take<uint8_t>(576);
+  LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(64), k_fp12_to_bytes, (const uint32_t*)f, (size_t)1, (size_t)0,
+         d_out);
+  uint8_t h_st = 0;
+  HIPC(hipMemcpyAsync(out576, d_out, 576, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipMemcpyAsync(&h_st, st, 1, hipMemcpyDeviceToHost, c->stream));
+  HIPC(hipStreamSynchronize(c->stream));
+  return h_st == ST_OK ? 0 : 1;
+}
+
+int bls381_final_verify(size_t k, const uint8_t* parts576) {
+  if (k == 0 || !parts576) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, 4 * (align256(576 * k) + align256(144 * 4 * k) + align256(k)) + 8192))) return rc;
+  Bump b(c->ws);
+  hipStream_t s = c->stream;
+  uint8_t* d_in = b.take<uint8_t>(576 * k);
+  uint32_t* f = b.take<uint32_t>(144 * k);
+  uint8_t* st = b.take<uint8_t>(k);
+  HIPC(hipMemcpyAsync(d_in, parts576, 576 * k, hipMemcpyHostToDevice, s));
+  HIPC(hipMemsetAsync(st, 0, k, s));
+  LAUNCH("fp12_from_bytes", s, dim3(grid_for(k)), dim3(KBLOCK), k_fp12_from_bytes, k, (const uint8_t*)d_in, f);
+  uint32_t* rf;
+  uint8_t* rst;
+  if ((rc = reduce_fp12(k, f, st, b, s, &rf, &rst))) return rc;
+  uint8_t* d_v = b.take<uint8_t>(1);
+  LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)rf,
+         (const uint8_t*)rst, d_v);
+  uint8_t v = 0;
+  HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return v;
+}
+
+// ---- aggregation
+static int agg_batch_impl(int is_g2, size_t ng, const uint32_t* offsets, size_t n_pts, const uint8_t* d_pts,
+                          uint8_t* d_out, int32_t* d_status, void* ws, hipStream_t s) {
+  AggPlan plan = plan_agg(ng, offsets);
+  const uint32_t* jac;
+  const uint8_t* bad;
+  size_t used = 0;
+  int rc;
+  (void)n_pts;
+  if (is_g2) {
+    if ((rc = run_agg<fp2_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
+    LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp2_t>, ng, jac, bad, d_out, d_status);
+  } else {
+    if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
+    LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
+  }
+  return 0;
+}
+
+static size_t agg_ws_bytes(int is_g2, size_t ng, const uint32_t* offsets) {
+  AggPlan plan = plan_agg(ng, offsets);
+  return agg_ws_size(plan, is_g2 ? 6 : 3);
+}
+
+size_t bls381_aggregate_pubkeys_batch_workspace_size(size_t n_groups, size_t n_pks) {
+  // worst case chunking: every group splits into ceil(size/CHUNK) chunks, plus levels
+  const size_t chunks = n_groups + n_pks / CHUNK_L1 + 1;
+  return 8192 + 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * 48) + align256(chunks));
+}
+
+int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_offsets, size_t n_pks,
+                                          const uint8_t* d_pks, uint8_t* d_out48, int32_t* d_status,
+                                          void* d_workspace, void* stream) {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n_groups == 0) return 0;
+  if (!h_offsets || !d_out48 || !d_status || !d_workspace) return BLS381_EARG;
+  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  return agg_batch_impl(0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace, s);
+}
+
+static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t* pts, uint8_t* out, int32_t* status) {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t bytes = is_g2 ? 96 : 48;
+  const size_t npts = offsets[ng];
+  const size_t need = align256(npts * bytes + 1) + align256(ng * bytes) + align256(ng * 4) + agg_ws_bytes(is_g2, ng, offsets) + 4096;
+  if ((rc = ensure_ws(c, need))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_pts = b.take<uint8_t>(npts * bytes + 1);
+  uint8_t* d_out = b.take<uint8_t>(ng * bytes);
+  int32_t* d_st = b.take<int32_t>(ng);
+  hipStream_t s = c->stream;
+  if (npts) HIPC(hipMemcpyAsync(d_pts, pts, npts * bytes, hipMemcpyHostToDevice, s));
+  if ((rc = agg_batch_impl(is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off), s))) return rc;
+  HIPC(hipMemcpyAsync(out, d_out, ng * bytes, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(status, d_st, ng * 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_aggregate_pubkeys_batch(size_t n_groups, const uint32_t* offsets, const uint8_t* pks, uint8_t* out48,
+                                   int32_t* status) {
+  if (n_groups == 0) return 0;
+  if (!offsets || !out48 || !status || (offsets[n_groups] && !pks)) return BLS381_EARG;
+  return agg_host(0, n_groups, offsets, pks, out48, status);
+}
+
+int bls381_aggregate_pubkeys(size_t n, const uint8_t* pks, uint8_t out[48]) {
+  if (!out || (n && !pks)) return BLS381_EARG;
+  uint32_t off[2] = {0, (uint32_t)n};
+  int32_t st = 0;
+  int rc = agg_host(0, 1, off, pks, out, &st);
+  return rc ? rc : st;
+}
+
+int bls381_aggregate_signatures(size_t n, const uint8_t* sigs, uint8_t out[96]) {
+  if (!out || (n && !sigs)) return BLS381_EARG;
+  uint32_t off[2] = {0, (uint32_t)n};
+  int32_t st = 0;
+  int rc = agg_host(1, 1, off, sigs, out, &st);
+  return rc ? rc : st;
+}
+
+// ---- single-item helpers (fixtures / reference API)
+int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const uint8_t dom8[8], uint8_t out[96]) {
+  if ((!msg && msg_len) || !sk || !dom8 || !out || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_msg = b.take<uint8_t>(msg_len + 1);
+  uint8_t* d_sk = b.take<uint8_t>(32);
+  uint8_t* d_dom = b.take<uint8_t>(8);
+  uint8_t* d_out = b.take<uint8_t>(96);
+  hipStream_t s = c->stream;
+  if (msg_len) HIPC(hipMemcpyAsync(d_msg, msg, msg_len, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sk, sk, 32, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_dom, dom8, 8, hipMemcpyHostToDevice, s));
+  LAUNCH("sign", s, dim3(1), dim3(KBLOCK), k_sign, (size_t)1, (const uint8_t*)d_msg, (uint32_t)msg_len,
+         (const uint8_t*)d_sk, (const uint8_t*)d_dom, d_out);
+  HIPC(hipMemcpyAsync(out, d_out, 96, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const uint8_t* dom8s, uint8_t* out96) {
+  if (n == 0) return 0;
+  if (!msgs32 || !sks || !dom8s || !out96) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, align256(32 * n) * 2 + align256(8 * n) + align256(96 * n) + 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_msg = b.take<uint8_t>(32 * n);
+  uint8_t* d_sk = b.take<uint8_t>(32 * n);
+  uint8_t* d_dom = b.take<uint8_t>(8 * n);
+  uint8_t* d_out = b.take<uint8_t>(96 * n);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_msg, msgs32, 32 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sk, sks, 32 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_dom, dom8s, 8 * n, hipMemcpyHostToDevice, s));
+  LAUNCH("sign", s, dim3(grid_for(n)), dim3(KBLOCK), k_sign, n, (const uint8_t*)d_msg, (uint32_t)32,
+         (const uint8_t*)d_sk, (const uint8_t*)d_dom, d_out);
+  HIPC(hipMemcpyAsync(out96, d_out, 96 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48) {
+  if (n == 0) return 0;
+  if (!sks || !out48) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, align256(32 * n) + align256(48 * n) + 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_sk = b.take<uint8_t>(32 * n);
+  uint8_t* d_out = b.take<uint8_t>(48 * n);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_sk, sks, 32 * n, hipMemcpyHostToDevice, s));
+  LAUNCH("privtopub", s, dim3(grid_for(n)), dim3(KBLOCK), k_privtopub, n, (const uint8_t*)d_sk, d_out);
+  HIPC(hipMemcpyAsync(out48, d_out, 48 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_privtopub(const uint8_t sk[32], uint8_t out[48]) {
+  if (!sk || !out) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_sk = b.take<uint8_t>(32);
+  uint8_t* d_out = b.take<uint8_t>(48);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_sk, sk, 32, hipMemcpyHostToDevice, s));
+  LAUNCH("privtopub", s, dim3(1), dim3(KBLOCK), k_privtopub, (size_t)1, (const uint8_t*)d_sk, d_out);
+  HIPC(hipMemcpyAsync(out, d_out, 48, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_hash_to_g2(const uint8_t* msg, size_t msg_len, const uint8_t dom8[8], uint8_t out_compressed[96],
+                      uint8_t out_affine[192]) {
+  if ((!msg && msg_len) || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_msg = b.take<uint8_t>(msg_len + 1);
+  uint8_t* d_dom = b.take<uint8_t>(8);
+  uint8_t* d_comp = b.take<uint8_t>(96);
+  uint8_t* d_aff = b.take<uint8_t>(192);
+  hipStream_t s = c->stream;
+  if (msg_len) HIPC(hipMemcpyAsync(d_msg, msg, msg_len, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_dom, dom8, 8, hipMemcpyHostToDevice, s));
+  LAUNCH("hash_to_g2", s, dim3(1), dim3(KBLOCK), k_hash_g2_out, (size_t)1, (const uint8_t*)d_msg, (uint32_t)msg_len,
+         (const uint8_t*)d_dom, d_comp, d_aff);
+  if (out_compressed) HIPC(hipMemcpyAsync(out_compressed, d_comp, 96, hipMemcpyDeviceToHost, s));
+  if (out_affine) HIPC(hipMemcpyAsync(out_affine, d_aff, 192, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const uint8_t* dom8s, uint8_t* out288) {
+  if (n == 0) return 0;
+  if (!msgs32 || !dom8s || !out288) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t scratch = (size_t)n * H2_BITS * 6 * 12 * 4;
+  if ((rc = ensure_ws(c, align256(32 * n) + align256(8 * n) + align256(288 * n) + align256(scratch) + 4096))) return rc;
+  Bump b(c->ws);
+  uint8_t* d_msgs = b.take<uint8_t>(32 * n);
+  uint8_t* d_doms = b.take<uint8_t>(8 * n);
+  uint8_t* d_out = b.take<uint8_t>(288 * n);
+  uint32_t* d_scr = b.take<uint32_t>(scratch / 4);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_msgs, msgs32, 32 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n, hipMemcpyHostToDevice, s));
+  LAUNCH("hash_to_g2_pyecc", s, dim3(grid_for(n, 64)), dim3(64), k_hash_g2_pyecc, n, (const uint8_t*)d_msgs,
+         (const uint8_t*)d_doms, d_scr, d_out);
+  HIPC(hipMemcpyAsync(out288, d_out, 288 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // extern "C"

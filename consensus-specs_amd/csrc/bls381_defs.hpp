@@ -1,0 +1,36 @@
+// Basic types and qualifiers shared by the gfx950 kernels and the host unit-test
+// build of the same arithmetic (DESIGN.md "One source, two compilers").
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define BLS_HD __host__ __device__
+#define BLS_INLINE __host__ __device__ __forceinline__
+#define BLS_NOINLINE __host__ __device__ __attribute__((noinline))
+#define BLS_CONST __device__ __constant__ static constexpr
+#else
+#define BLS_HD
+#define BLS_INLINE inline __attribute__((always_inline))
+#define BLS_NOINLINE __attribute__((noinline))
+#define BLS_CONST static constexpr
+#endif
+
+namespace bls381 {
+
+// Fp element: 12 x 32-bit limbs, little-endian, Montgomery form (R = 2^384)
+struct fp_t { uint32_t w[12]; };
+// Fp2 = Fp[u]/(u^2+1): c0 + c1 u
+struct fp2_t { fp_t c0, c1; };
+// Fp6 = Fp2[v]/(v^3 - (1+u))
+struct fp6_t { fp2_t c0, c1, c2; };
+// Fp12 = Fp6[w]/(w^2 - v): c0 + c1 w
+struct fp12_t { fp6_t c0, c1; };
+
+// Jacobian points (X/Z^2, Y/Z^3); Z == 0 is the point at infinity
+struct g1_jac { fp_t x, y, z; };
+struct g2_jac { fp2_t x, y, z; };
+struct g1_aff { fp_t x, y; };
+struct g2_aff { fp2_t x, y; };
+
+}  // namespace bls381

@@ -1,0 +1,479 @@
+// BLS12-381 base field Fp and the tower Fp2 / Fp6 / Fp12.
+//
+// Fp: 12 x u32 limbs, Montgomery form R = 2^384.  Multiplication is the
+// "no-carry" CIOS variant (valid because q's top limb 0x1a0111ea < 2^31 - 2):
+// one v_mad_u64_u32 per 32x32 partial product, limbs stay in VGPRs.
+// Tower (DESIGN.md "Data layout"):  Fp2 = Fp[u]/(u^2+1),
+// Fp6 = Fp2[v]/(v^3 - (1+u)),  Fp12 = Fp6[w]/(w^2 - v)  (w^6 = 1+u).
+// Algorithms are mirrored 1:1 by oracle/tower_model.py (test infrastructure).
+#pragma once
+#include "bls381_defs.hpp"
+#include "bls381_consts.hpp"
+
+namespace bls381 {
+
+#if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
+// host op-count build (tools / bench roofline): Fp multiplications executed
+inline thread_local uint64_t g_fp_mul_count = 0;
+#define BLS_COUNT_FP_MUL() (++g_fp_mul_count)
+#else
+#define BLS_COUNT_FP_MUL() ((void)0)
+#endif
+
+// ----------------------------------------------------------------- Fp -----
+BLS_INLINE fp_t fp_zero() { fp_t r; for (int i = 0; i < 12; ++i) r.w[i] = 0; return r; }
+BLS_INLINE fp_t fp_one() { return FP_ONE_M; }
+
+BLS_INLINE bool fp_is_zero(const fp_t& a) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.w[i];
+  return acc == 0;
+}
+
+BLS_INLINE bool fp_eq(const fp_t& a, const fp_t& b) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc |= a.w[i] ^ b.w[i];
+  return acc == 0;
+}
+
+// r = s - q if s >= q else s   (s < 2q)
+BLS_INLINE fp_t fp_reduce_once(const fp_t& s) {
+  fp_t d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)s.w[i] - Q_LIMBS[i] - br;
+    d.w[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.w[i] = br ? s.w[i] : d.w[i];
+  return r;
+}
+
+BLS_INLINE fp_t fp_add(const fp_t& a, const fp_t& b) {
+  fp_t s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.w[i] + b.w[i] + c;
+    s.w[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return fp_reduce_once(s);
+}
+
+BLS_INLINE fp_t fp_sub(const fp_t& a, const fp_t& b) {
+  fp_t d;
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.w[i] - b.w[i] - br;
+    d.w[i] = (uint32_t)t;
+    br = (uint32_t)(t >> 63);
+  }
+  // if borrow: d += q
+  fp_t e;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)d.w[i] + (br ? Q_LIMBS[i] : 0u) + c;
+    e.w[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return e;
+}
+
+BLS_INLINE fp_t fp_neg(const fp_t& a) {
+  fp_t z = fp_zero();
+  return fp_sub(z, a);
+}
+
+BLS_INLINE fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
+
+// a / 2 mod q
+BLS_INLINE fp_t fp_half(const fp_t& a) {
+  const uint32_t odd = a.w[0] & 1u;
+  fp_t s;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.w[i] + (odd ? Q_LIMBS[i] : 0u) + c;
+    s.w[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) r.w[i] = (s.w[i] >> 1) | (s.w[i + 1] << 31);
+  r.w[11] = (s.w[11] >> 1) | (c << 31);
+  return r;
+}
+
+// Montgomery product a * b * R^-1 mod q, inputs < q, output < q.
+BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) {
+  BLS_COUNT_FP_MUL();
+  uint32_t t[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint32_t bi = b.w[i];
+    uint64_t s = (uint64_t)a.w[0] * bi + t[0];
+    uint32_t A = (uint32_t)(s >> 32);
+    const uint32_t t0 = (uint32_t)s;
+    const uint32_t m = t0 * Q_INV32;
+    uint64_t s2 = (uint64_t)m * Q_LIMBS[0] + t0;
+    uint32_t C = (uint32_t)(s2 >> 32);
+#pragma unroll
+    for (int j = 1; j < 12; ++j) {
+      s = (uint64_t)a.w[j] * bi + t[j] + A;
+      A = (uint32_t)(s >> 32);
+      s2 = (uint64_t)m * Q_LIMBS[j] + (uint32_t)s + C;
+      C = (uint32_t)(s2 >> 32);
+      t[j - 1] = (uint32_t)s2;
+    }
+    t[11] = C + A;
+  }
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) r.w[i] = t[i];
+  return fp_reduce_once(r);
+}
+
+BLS_INLINE fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
+
+BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
+  // k in {2,3,4,8,...}: small constant multiples by addition chains
+  fp_t r = a;
+  fp_t acc = fp_zero();
+  bool first = true;
+  while (k) {
+    if (k & 1) { acc = first ? r : fp_add(acc, r); first = false; }
+    k >>= 1;
+    if (k) r = fp_dbl(r);
+  }
+  return acc;
+}
+
+// left-to-right square-and-multiply over a 12-limb little-endian exponent
+BLS_HD inline fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
+  fp_t r = FP_ONE_M;
+  for (int i = nbits - 1; i >= 0; --i) {
+    r = fp_sqr(r);
+    if ((e[i >> 5] >> (i & 31)) & 1u) r = fp_mul(r, a);
+  }
+  return r;
+}
+
+BLS_HD inline fp_t fp_inv(const fp_t& a) { return fp_pow_limbs(a, EXP_INV, 381); }
+
+// returns true and sets r when a is a square; r = a^((q+1)/4)
+BLS_HD inline bool fp_sqrt(fp_t& r, const fp_t& a) {
+  r = fp_pow_limbs(a, EXP_SQRT, 379);
+  return fp_eq(fp_sqr(r), a);
+}
+
+BLS_INLINE fp_t fp_to_mont(const fp_t& plain) { return fp_mul(plain, FP_R2); }
+BLS_INLINE fp_t fp_from_mont(const fp_t& m) {
+  fp_t one = fp_zero();
+  one.w[0] = 1;
+  return fp_mul(m, one);
+}
+
+// plain (non-Montgomery) comparisons and byte codecs
+BLS_INLINE bool fp_plain_lt_q(const fp_t& a) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)a.w[i] - Q_LIMBS[i] - br;
+    br = (uint32_t)(t >> 63);
+  }
+  return br != 0;
+}
+
+// a > b for plain values
+BLS_INLINE bool fp_plain_gt(const fp_t& a, const fp_t& b) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)b.w[i] - a.w[i] - br;
+    br = (uint32_t)(t >> 63);
+  }
+  return br != 0;  // b - a borrows  <=>  b < a
+}
+
+// (2*y) // q == 1  <=>  2y >= q, for plain y < q (spec a_flag, bls_signature.md:52)
+BLS_INLINE bool fp_plain_is_upper_half(const fp_t& y) {
+  uint32_t c = 0;
+  fp_t s;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint64_t t = (uint64_t)y.w[i] + y.w[i] + c;
+    s.w[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+  return !fp_plain_lt_q(s);
+}
+
+// 48 big-endian bytes -> plain limbs (no reduction)
+BLS_INLINE fp_t fp_plain_from_be48(const uint8_t* p) {
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const uint8_t* b = p + 44 - 4 * i;
+    r.w[i] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  }
+  return r;
+}
+
+BLS_INLINE void fp_plain_to_be48(uint8_t* p, const fp_t& a) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    uint8_t* b = p + 44 - 4 * i;
+    b[0] = (uint8_t)(a.w[i] >> 24);
+    b[1] = (uint8_t)(a.w[i] >> 16);
+    b[2] = (uint8_t)(a.w[i] >> 8);
+    b[3] = (uint8_t)a.w[i];
+  }
+}
+
+// ---------------------------------------------------------------- Fp2 -----
+BLS_INLINE fp2_t fp2_zero() { fp2_t r; r.c0 = fp_zero(); r.c1 = fp_zero(); return r; }
+BLS_INLINE fp2_t fp2_one() { fp2_t r; r.c0 = FP_ONE_M; r.c1 = fp_zero(); return r; }
+BLS_INLINE bool fp2_is_zero(const fp2_t& a) { return fp_is_zero(a.c0) && fp_is_zero(a.c1); }
+BLS_INLINE bool fp2_eq(const fp2_t& a, const fp2_t& b) { return fp_eq(a.c0, b.c0) && fp_eq(a.c1, b.c1); }
+BLS_INLINE fp2_t fp2_add(const fp2_t& a, const fp2_t& b) { fp2_t r; r.c0 = fp_add(a.c0, b.c0); r.c1 = fp_add(a.c1, b.c1); return r; }
+BLS_INLINE fp2_t fp2_sub(const fp2_t& a, const fp2_t& b) { fp2_t r; r.c0 = fp_sub(a.c0, b.c0); r.c1 = fp_sub(a.c1, b.c1); return r; }
+BLS_INLINE fp2_t fp2_neg(const fp2_t& a) { fp2_t r; r.c0 = fp_neg(a.c0); r.c1 = fp_neg(a.c1); return r; }
+BLS_INLINE fp2_t fp2_dbl(const fp2_t& a) { return fp2_add(a, a); }
+BLS_INLINE fp2_t fp2_half(const fp2_t& a) { fp2_t r; r.c0 = fp_half(a.c0); r.c1 = fp_half(a.c1); return r; }
+BLS_INLINE fp2_t fp2_conj(const fp2_t& a) { fp2_t r; r.c0 = a.c0; r.c1 = fp_neg(a.c1); return r; }
+BLS_INLINE fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { fp2_t r; r.c0 = fp_mul(a.c0, b); r.c1 = fp_mul(a.c1, b); return r; }
+
+BLS_INLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
+  const fp_t t0 = fp_mul(a.c0, b.c0);
+  const fp_t t1 = fp_mul(a.c1, b.c1);
+  const fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  fp2_t r;
+  r.c0 = fp_sub(t0, t1);
+  r.c1 = fp_sub(fp_sub(t2, t0), t1);
+  return r;
+}
+
+BLS_INLINE fp2_t fp2_sqr(const fp2_t& a) {
+  fp2_t r;
+  r.c0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  const fp_t t = fp_mul(a.c0, a.c1);
+  r.c1 = fp_add(t, t);
+  return r;
+}
+
+// multiply by xi = 1 + u
+BLS_INLINE fp2_t fp2_mul_xi(const fp2_t& a) {
+  fp2_t r;
+  r.c0 = fp_sub(a.c0, a.c1);
+  r.c1 = fp_add(a.c0, a.c1);
+  return r;
+}
+
+BLS_INLINE fp2_t fp2_mul_small(const fp2_t& a, int k) {
+  fp2_t r; r.c0 = fp_mul_small(a.c0, k); r.c1 = fp_mul_small(a.c1, k); return r;
+}
+
+BLS_HD inline fp2_t fp2_inv(const fp2_t& a) {
+  const fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  const fp_t ni = fp_inv(n);
+  fp2_t r;
+  r.c0 = fp_mul(a.c0, ni);
+  r.c1 = fp_neg(fp_mul(a.c1, ni));
+  return r;
+}
+
+// Complex-method square root for q = 3 mod 4 (DESIGN.md "Square roots").
+// Returns false when a is a non-square.  Which of the two roots is returned
+// is unspecified; callers apply the spec's selection rule.
+BLS_HD inline bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
+  if (fp_is_zero(a.c1)) {
+    fp_t s;
+    if (fp_sqrt(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
+    if (fp_sqrt(s, fp_neg(a.c0))) { r.c0 = fp_zero(); r.c1 = s; return true; }
+    return false;
+  }
+  const fp_t alpha = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
+  fp_t gamma;
+  if (!fp_sqrt(gamma, alpha)) return false;
+  const fp_t delta = fp_half(fp_add(a.c0, gamma));
+  const fp_t t = fp_pow_limbs(delta, EXP_SQRT, 379);
+  const fp_t inv2t = fp_inv(fp_dbl(t));
+  const fp_t other = fp_mul(a.c1, inv2t);
+  if (fp_eq(fp_sqr(t), delta)) { r.c0 = t; r.c1 = other; }
+  else { r.c0 = other; r.c1 = t; }
+  return true;
+}
+
+// ---------------------------------------------------------------- Fp6 -----
+BLS_INLINE fp6_t fp6_zero() { fp6_t r; r.c0 = fp2_zero(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
+BLS_INLINE fp6_t fp6_one() { fp6_t r; r.c0 = fp2_one(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
+BLS_INLINE fp6_t fp6_add(const fp6_t& a, const fp6_t& b) { fp6_t r; r.c0 = fp2_add(a.c0, b.c0); r.c1 = fp2_add(a.c1, b.c1); r.c2 = fp2_add(a.c2, b.c2); return r; }
+BLS_INLINE fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) { fp6_t r; r.c0 = fp2_sub(a.c0, b.c0); r.c1 = fp2_sub(a.c1, b.c1); r.c2 = fp2_sub(a.c2, b.c2); return r; }
+BLS_INLINE fp6_t fp6_neg(const fp6_t& a) { fp6_t r; r.c0 = fp2_neg(a.c0); r.c1 = fp2_neg(a.c1); r.c2 = fp2_neg(a.c2); return r; }
+BLS_INLINE bool fp6_is_zero(const fp6_t& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }
+
+BLS_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
+  const fp2_t t0 = fp2_mul(a.c0, b.c0);
+  const fp2_t t1 = fp2_mul(a.c1, b.c1);
+  const fp2_t t2 = fp2_mul(a.c2, b.c2);
+  fp6_t r;
+  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
+  r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  return r;
+}
+
+BLS_INLINE fp6_t fp6_mul_by_v(const fp6_t& a) {
+  fp6_t r; r.c0 = fp2_mul_xi(a.c2); r.c1 = a.c0; r.c2 = a.c1; return r;
+}
+
+BLS_HD inline fp6_t fp6_inv(const fp6_t& a) {
+  const fp2_t c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  const fp2_t c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  const fp2_t c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  const fp2_t t = fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2))));
+  const fp2_t ti = fp2_inv(t);
+  fp6_t r;
+  r.c0 = fp2_mul(c0, ti);
+  r.c1 = fp2_mul(c1, ti);
+  r.c2 = fp2_mul(c2, ti);
+  return r;
+}
+
+// ---------------------------------------------------------------- Fp12 ----
+BLS_INLINE fp12_t fp12_one() { fp12_t r; r.c0 = fp6_one(); r.c1 = fp6_zero(); return r; }
+
+BLS_INLINE bool fp12_is_one(const fp12_t& a) {
+  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp6_is_zero(a.c1);
+}
+
+BLS_INLINE bool fp12_eq(const fp12_t& a, const fp12_t& b) {
+  return fp2_eq(a.c0.c0, b.c0.c0) && fp2_eq(a.c0.c1, b.c0.c1) && fp2_eq(a.c0.c2, b.c0.c2) &&
+         fp2_eq(a.c1.c0, b.c1.c0) && fp2_eq(a.c1.c1, b.c1.c1) && fp2_eq(a.c1.c2, b.c1.c2);
+}
+
+BLS_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
+  const fp6_t ac = fp6_mul(a.c0, b.c0);
+  const fp6_t bd = fp6_mul(a.c1, b.c1);
+  fp12_t r;
+  r.c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), ac), bd);
+  r.c0 = fp6_add(ac, fp6_mul_by_v(bd));
+  return r;
+}
+
+// complex squaring: (a + b w)^2 = (a^2 + v b^2) + 2ab w
+//   = ((a + b)(a + v b) - ab - v ab) + 2ab w
+BLS_NOINLINE fp12_t fp12_sqr(const fp12_t& f) {
+  const fp6_t ab = fp6_mul(f.c0, f.c1);
+  const fp6_t t = fp6_mul(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
+  fp12_t r;
+  r.c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_by_v(ab));
+  r.c1 = fp6_add(ab, ab);
+  return r;
+}
+
+BLS_INLINE fp12_t fp12_conj(const fp12_t& a) { fp12_t r; r.c0 = a.c0; r.c1 = fp6_neg(a.c1); return r; }
+
+BLS_HD inline fp12_t fp12_inv(const fp12_t& f) {
+  const fp6_t t = fp6_sub(fp6_mul(f.c0, f.c0), fp6_mul_by_v(fp6_mul(f.c1, f.c1)));
+  const fp6_t ti = fp6_inv(t);
+  fp12_t r;
+  r.c0 = fp6_mul(f.c0, ti);
+  r.c1 = fp6_neg(fp6_mul(f.c1, ti));
+  return r;
+}
+
+// f^(q^p), p in {1,2,3}; coefficient of w^k picks up gamma[p][k] (and conj for odd p)
+BLS_HD inline fp12_t fp12_frob(const fp12_t& f, int p) {
+  const fp2_t* g = FROB_GAMMA_M[p - 1];
+  const bool odd = (p & 1) != 0;
+  auto fr = [&](const fp2_t& c, int k) -> fp2_t {
+    const fp2_t cc = odd ? fp2_conj(c) : c;
+    return k == 0 ? cc : fp2_mul(cc, g[k]);
+  };
+  fp12_t r;
+  r.c0.c0 = fr(f.c0.c0, 0);
+  r.c0.c1 = fr(f.c0.c1, 2);
+  r.c0.c2 = fr(f.c0.c2, 4);
+  r.c1.c0 = fr(f.c1.c0, 1);
+  r.c1.c1 = fr(f.c1.c1, 3);
+  r.c1.c2 = fr(f.c1.c2, 5);
+  return r;
+}
+
+// sparse product f * (c0 + c1 v + c2 v w): 13 Fp2 multiplications
+BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2_t& c1, const fp2_t& c2) {
+  const fp6_t& a = f.c0;
+  const fp6_t& b = f.c1;
+  // aA, A = c0 + c1 v
+  fp6_t aA;
+  {
+    const fp2_t t0 = fp2_mul(a.c0, c0);
+    const fp2_t t1 = fp2_mul(a.c1, c1);
+    aA.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, c1)));
+    aA.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(c0, c1)), t0), t1);
+    aA.c2 = fp2_add(t1, fp2_mul(a.c2, c0));
+  }
+  // bB, B = c2 v
+  fp6_t bB;
+  bB.c0 = fp2_mul_xi(fp2_mul(b.c2, c2));
+  bB.c1 = fp2_mul(b.c0, c2);
+  bB.c2 = fp2_mul(b.c1, c2);
+  // (a + b)(A + B), A + B = c0 + (c1 + c2) v
+  const fp6_t s = fp6_add(a, b);
+  const fp2_t d1 = fp2_add(c1, c2);
+  fp6_t m;
+  {
+    const fp2_t t0 = fp2_mul(s.c0, c0);
+    const fp2_t t1 = fp2_mul(s.c1, d1);
+    m.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(s.c2, d1)));
+    m.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(s.c0, s.c1), fp2_add(c0, d1)), t0), t1);
+    m.c2 = fp2_add(t1, fp2_mul(s.c2, c0));
+  }
+  fp12_t r;
+  r.c0 = fp6_add(aA, fp6_mul_by_v(bB));
+  r.c1 = fp6_sub(fp6_sub(m, aA), bB);
+  return r;
+}
+
+// Granger-Scott squaring in the cyclotomic subgroup.  View Fp12 as
+// Fp4[w]/(w^3 - z), Fp4 = Fp2[z]/(z^2 - xi), z = w^3:
+//   f = A + B w + C w^2,  A = a0 + b1 z,  B = b0 + a2 z,  C = a1 + b2 z
+//   A' = 3A^2 - 2 conj(A),  B' = 3 z C^2 + 2 conj(B),  C' = 3 B^2 - 2 conj(C)
+BLS_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
+  const fp2_t& a0 = f.c0.c0; const fp2_t& a1 = f.c0.c1; const fp2_t& a2 = f.c0.c2;
+  const fp2_t& b0 = f.c1.c0; const fp2_t& b1 = f.c1.c1; const fp2_t& b2 = f.c1.c2;
+  auto sq4 = [](const fp2_t& x0, const fp2_t& x1, fp2_t& r0, fp2_t& r1) {
+    const fp2_t t0 = fp2_sqr(x0);
+    const fp2_t t1 = fp2_sqr(x1);
+    r0 = fp2_add(t0, fp2_mul_xi(t1));
+    r1 = fp2_sub(fp2_sqr(fp2_add(x0, x1)), fp2_add(t0, t1));
+  };
+  fp2_t A0, A1, B0, B1, C0, C1;
+  sq4(a0, b1, A0, A1);
+  sq4(b0, a2, B0, B1);
+  sq4(a1, b2, C0, C1);
+  fp12_t r;
+  // A'
+  r.c0.c0 = fp2_sub(fp2_mul_small(A0, 3), fp2_dbl(a0));
+  r.c1.c1 = fp2_add(fp2_mul_small(A1, 3), fp2_dbl(b1));
+  // B' = 3 z C^2 + 2 conj(B);  z (C0 + C1 z) = xi C1 + C0 z
+  r.c1.c0 = fp2_add(fp2_mul_small(fp2_mul_xi(C1), 3), fp2_dbl(b0));
+  r.c0.c2 = fp2_sub(fp2_mul_small(C0, 3), fp2_dbl(a2));
+  // C'
+  r.c0.c1 = fp2_sub(fp2_mul_small(B0, 3), fp2_dbl(a1));
+  r.c1.c2 = fp2_add(fp2_mul_small(B1, 3), fp2_dbl(b2));
+  return r;
+}
+
+}  // namespace bls381

@@ -1,0 +1,132 @@
+// SHA-256 (specs/core/0_beacon-chain.md:591-595) and the spec's try-and-increment
+// hash_to_G2 (specs/bls_signature.md:68-87) on the device.
+#pragma once
+#include "bls381_curve.hpp"
+
+namespace bls381 {
+
+BLS_CONST uint32_t SHA256_K[64] = {
+    0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
+    0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
+    0xe49b69c1u, 0xefbe4786u, 0x0fc19dc6u, 0x240ca1ccu, 0x2de92c6fu, 0x4a7484aau, 0x5cb0a9dcu, 0x76f988dau,
+    0x983e5152u, 0xa831c66du, 0xb00327c8u, 0xbf597fc7u, 0xc6e00bf3u, 0xd5a79147u, 0x06ca6351u, 0x14292967u,
+    0x27b70a85u, 0x2e1b2138u, 0x4d2c6dfcu, 0x53380d13u, 0x650a7354u, 0x766a0abbu, 0x81c2c92eu, 0x92722c85u,
+    0xa2bfe8a1u, 0xa81a664bu, 0xc24b8b70u, 0xc76c51a3u, 0xd192e819u, 0xd6990624u, 0xf40e3585u, 0x106aa070u,
+    0x19a4c116u, 0x1e376c08u, 0x2748774cu, 0x34b0bcb5u, 0x391c0cb3u, 0x4ed8aa4au, 0x5b9cca4fu, 0x682e6ff3u,
+    0x748f82eeu, 0x78a5636fu, 0x84c87814u, 0x8cc70208u, 0x90befffau, 0xa4506cebu, 0xbef9a3f7u, 0xc67178f2u};
+
+BLS_INLINE uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+
+// one compression of a 16-word big-endian block into state h[8]
+BLS_HD inline void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
+  uint32_t w[64];
+  for (int i = 0; i < 16; ++i) w[i] = blk[i];
+  for (int i = 16; i < 64; ++i) {
+    const uint32_t s0 = rotr32(w[i - 15], 7) ^ rotr32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    const uint32_t s1 = rotr32(w[i - 2], 17) ^ rotr32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = hh + S1 + ch + SHA256_K[i] + w[i];
+    const uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// SHA-256 of an arbitrary byte string (multi-block), digest as 8 big-endian words
+BLS_HD inline void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t bitlen = (uint64_t)len * 8;
+  const uint32_t nblocks = (len + 9 + 63) / 64;
+  for (uint32_t bi = 0; bi < nblocks; ++bi) {
+    uint32_t blk[16];
+    for (int wi = 0; wi < 16; ++wi) {
+      uint32_t word = 0;
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t pos = (uint64_t)bi * 64 + wi * 4 + k;
+        uint8_t byte;
+        if (pos < len) byte = msg[pos];
+        else if (pos == len) byte = 0x80;
+        else if (pos >= (uint64_t)nblocks * 64 - 8) byte = (uint8_t)(bitlen >> (8 * (nblocks * 64 - 1 - pos)));
+        else byte = 0;
+        word = (word << 8) | byte;
+      }
+      blk[wi] = word;
+    }
+    sha256_compress(h, blk);
+  }
+  for (int i = 0; i < 8; ++i) out[i] = h[i];
+}
+
+// 8 big-endian digest words -> plain Fp limbs (256-bit value < q)
+BLS_INLINE fp_t fp_plain_from_digest(const uint32_t d[8]) {
+  fp_t r = fp_zero();
+  for (int i = 0; i < 8; ++i) r.w[i] = d[7 - i];
+  return r;
+}
+
+// spec root selection (bls_signature.md:91,107): keep the root whose imaginary
+// part is the larger of {y_im, q - y_im}, ties (y_im == 0) broken on the real part.
+BLS_INLINE fp2_t g2_select_root(const fp2_t& y) {
+  return g2_y_flag(y) ? y : fp2_neg(y);
+}
+
+// try-and-increment part of hash_to_G2 (bls_signature.md:74-86), before the cofactor.
+// msg may be any length (py_ecc hashes any bytes); dom8 = 8 domain bytes.
+BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, uint32_t mlen,
+                                       const uint8_t dom8[8], uint8_t* scratch /* mlen + 9 */) {
+  for (uint32_t i = 0; i < mlen; ++i) scratch[i] = msg[i];
+  for (int i = 0; i < 8; ++i) scratch[mlen + i] = dom8[i];
+  uint32_t d[8];
+  scratch[mlen + 8] = 1;
+  sha256(d, scratch, mlen + 9);
+  fp2_t x;
+  x.c0 = fp_to_mont(fp_plain_from_digest(d));
+  scratch[mlen + 8] = 2;
+  sha256(d, scratch, mlen + 9);
+  x.c1 = fp_to_mont(fp_plain_from_digest(d));
+  int trials = 0;
+  while (true) {
+    ++trials;
+    const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
+    fp2_t y;
+    if (fp2_sqrt(y, rhs)) {
+      out.x = x;
+      out.y = g2_select_root(y);
+      return trials;
+    }
+    x.c0 = fp_add(x.c0, FP_ONE_M);
+  }
+}
+
+// [h2] P with the spec's G2_cofactor (bls_signature.md:71), signed-binary (NAF) digits
+BLS_HD inline jac_t<fp2_t> g2_mul_cofactor(const aff_t<fp2_t>& p) {
+  aff_t<fp2_t> np;
+  np.x = p.x;
+  np.y = fp2_neg(p.y);
+  jac_t<fp2_t> r = jac_from_aff(p);   // leading NAF digit is +1
+  for (int i = 1; i < H2_NAF_LEN; ++i) {
+    r = jac_dbl(r);
+    const int dg = H2_NAF[i];
+    if (dg > 0) r = jac_add_aff(r, p);
+    else if (dg < 0) r = jac_add_aff(r, np);
+  }
+  return r;
+}
+
+// full hash_to_G2 for a 32-byte message; returns false only if the result is infinity
+BLS_HD inline bool hash_to_g2_aff(aff_t<fp2_t>& out, const uint8_t msg[32], const uint8_t dom8[8]) {
+  uint8_t scratch[41];
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msg, 32, dom8, scratch);
+  return jac_to_aff(out, g2_mul_cofactor(c));
+}
+
+}  // namespace bls381

@@ -1,0 +1,471 @@
+// gfx950 kernels of the BLS12-381 engine.  One work item per lane; every
+// intermediate lives in HBM in structure-of-arrays, limb-major layout
+// (limb k of component c of item i at base[(c*12 + k) * n + i]) so that each
+// limb load/store of a wavefront is one contiguous 256-byte access
+// (DESIGN.md "Data layout in HBM").
+#pragma once
+#include "bls381_hash.hpp"
+#include "bls381_pairing.hpp"
+
+namespace bls381 {
+
+enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2 };
+
+constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
+
+// ------------------------------------------------------------ SoA access --
+__device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < 12; ++k) r.w[k] = p[(size_t)(c * 12 + k) * n + i];
+  return r;
+}
+__device__ __forceinline__ void soa_st(uint32_t* __restrict__ p, size_t n, size_t i, int c, const fp_t& a) {
+#pragma unroll
+  for (int k = 0; k < 12; ++k) p[(size_t)(c * 12 + k) * n + i] = a.w[k];
+}
+__device__ __forceinline__ fp2_t soa_ld2(const uint32_t* p, size_t n, size_t i, int c) {
+  fp2_t r; r.c0 = soa_ld(p, n, i, c); r.c1 = soa_ld(p, n, i, c + 1); return r;
+}
+__device__ __forceinline__ void soa_st2(uint32_t* p, size_t n, size_t i, int c, const fp2_t& a) {
+  soa_st(p, n, i, c, a.c0); soa_st(p, n, i, c + 1, a.c1);
+}
+__device__ __forceinline__ aff_t<fp_t> soa_ld_g1(const uint32_t* p, size_t n, size_t i) {
+  aff_t<fp_t> a; a.x = soa_ld(p, n, i, 0); a.y = soa_ld(p, n, i, 1); return a;
+}
+__device__ __forceinline__ void soa_st_g1(uint32_t* p, size_t n, size_t i, const aff_t<fp_t>& a) {
+  soa_st(p, n, i, 0, a.x); soa_st(p, n, i, 1, a.y);
+}
+__device__ __forceinline__ aff_t<fp2_t> soa_ld_g2(const uint32_t* p, size_t n, size_t i) {
+  aff_t<fp2_t> a; a.x = soa_ld2(p, n, i, 0); a.y = soa_ld2(p, n, i, 2); return a;
+}
+__device__ __forceinline__ void soa_st_g2(uint32_t* p, size_t n, size_t i, const aff_t<fp2_t>& a) {
+  soa_st2(p, n, i, 0, a.x); soa_st2(p, n, i, 2, a.y);
+}
+__device__ __forceinline__ fp12_t soa_ld12(const uint32_t* p, size_t n, size_t i) {
+  fp12_t f;
+  f.c0.c0 = soa_ld2(p, n, i, 0); f.c0.c1 = soa_ld2(p, n, i, 2); f.c0.c2 = soa_ld2(p, n, i, 4);
+  f.c1.c0 = soa_ld2(p, n, i, 6); f.c1.c1 = soa_ld2(p, n, i, 8); f.c1.c2 = soa_ld2(p, n, i, 10);
+  return f;
+}
+__device__ __forceinline__ void soa_st12(uint32_t* p, size_t n, size_t i, const fp12_t& f) {
+  soa_st2(p, n, i, 0, f.c0.c0); soa_st2(p, n, i, 2, f.c0.c1); soa_st2(p, n, i, 4, f.c0.c2);
+  soa_st2(p, n, i, 6, f.c1.c0); soa_st2(p, n, i, 8, f.c1.c1); soa_st2(p, n, i, 10, f.c1.c2);
+}
+template <class F> struct soa_jac;
+template <> struct soa_jac<fp_t> {
+  static constexpr int NC = 3;
+  __device__ static jac_t<fp_t> ld(const uint32_t* p, size_t n, size_t i) {
+    jac_t<fp_t> r; r.x = soa_ld(p, n, i, 0); r.y = soa_ld(p, n, i, 1); r.z = soa_ld(p, n, i, 2); return r;
+  }
+  __device__ static void st(uint32_t* p, size_t n, size_t i, const jac_t<fp_t>& a) {
+    soa_st(p, n, i, 0, a.x); soa_st(p, n, i, 1, a.y); soa_st(p, n, i, 2, a.z);
+  }
+};
+template <> struct soa_jac<fp2_t> {
+  static constexpr int NC = 6;
+  __device__ static jac_t<fp2_t> ld(const uint32_t* p, size_t n, size_t i) {
+    jac_t<fp2_t> r; r.x = soa_ld2(p, n, i, 0); r.y = soa_ld2(p, n, i, 2); r.z = soa_ld2(p, n, i, 4); return r;
+  }
+  __device__ static void st(uint32_t* p, size_t n, size_t i, const jac_t<fp2_t>& a) {
+    soa_st2(p, n, i, 0, a.x); soa_st2(p, n, i, 2, a.y); soa_st2(p, n, i, 4, a.z);
+  }
+};
+
+__device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict__ src, int len) {
+  for (int k = 0; k < len; ++k) dst[k] = src[k];
+}
+
+// --------------------------------------------------------- decode kernels --
+// pubkeys -> affine G1 (SoA 2 Fp) + status; optional subgroup check
+__global__ void __launch_bounds__(KBLOCK) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
+                                                     uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                     int check_subgroup) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[48];
+  ld_bytes(b, pks + 48 * i, 48);
+  aff_t<fp_t> a;
+  int s = g1_decompress(a, b);
+  if (s == PT_OK && check_subgroup && !g1_in_subgroup(a)) s = PT_BAD;
+  st[i] = (uint8_t)s;
+  if (s == PT_OK) soa_st_g1(out, n, i, a);
+}
+
+// signatures -> affine G2 (SoA 4 Fp) + status; optional subgroup check
+__global__ void __launch_bounds__(KBLOCK) k_decode_g2(size_t n, const uint8_t* __restrict__ sigs,
+                                                     uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                     int check_subgroup) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t b[96];
+  ld_bytes(b, sigs + 96 * i, 96);
+  aff_t<fp2_t> a;
+  int s = g2_decompress(a, b);
+  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = PT_BAD;
+  st[i] = (uint8_t)s;
+  if (s == PT_OK) soa_st_g2(out, n, i, a);
+}
+
+// (msg, dom8) -> hash_to_G2 affine (SoA 4 Fp).  dom_stride 0 = one shared domain.
+__global__ void __launch_bounds__(KBLOCK) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                   const uint8_t* __restrict__ doms, int dom_stride,
+                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t scratch[BLS381_MSG_MAX + 9];
+  uint8_t dom[8];
+  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  aff_t<fp2_t> h;
+  const bool fin = jac_to_aff(h, g2_mul_cofactor(c));
+  if (st) st[i] = fin ? ST_OK : ST_INF;
+  if (fin) soa_st_g2(out, n, i, h);
+}
+
+// --------------------------------------------------------- verify kernels --
+// One bls_verify per lane: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
+// infinity short-circuit of py_ecc's pairing (a pair with an infinite point is 1).
+__global__ void __launch_bounds__(KBLOCK) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
+                                                         const uint8_t* __restrict__ sig_st,
+                                                         const uint32_t* __restrict__ pk_aff,
+                                                         const uint8_t* __restrict__ pk_st,
+                                                         const uint32_t* __restrict__ h_aff,
+                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t ss = sig_st[i], ps = pk_st[i];
+  if (ss == ST_BAD || ps == ST_BAD) { st_out[i] = ST_BAD; return; }
+  aff_t<fp2_t> Q[2];
+  g1_line_pre P[2];
+  int np = 0;
+  if (ss == ST_OK) {
+    Q[np] = soa_ld_g2(sig_aff, n, i);
+    aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+    P[np] = g1_prepare(ng);
+    ++np;
+  }
+  if (ps == ST_OK) {
+    Q[np] = soa_ld_g2(h_aff, n, i);
+    P[np] = g1_prepare(soa_ld_g1(pk_aff, n, i));
+    ++np;
+  }
+  fp12_t f;
+  if (np == 2) f = miller_loop_n<2>(Q, P);
+  else if (np == 1) f = miller_loop_n<1>(Q, P);
+  else f = fp12_one();
+  soa_st12(f_out, n, i, f);
+  st_out[i] = ST_OK;
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
+                                                             const uint8_t* __restrict__ st,
+                                                             uint8_t* __restrict__ verdict) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (st[i] != ST_OK) { verdict[i] = 0; return; }
+  const fp12_t f = soa_ld12(f_in, n, i);
+  verdict[i] = fp12_is_one(final_exp(f)) ? 1 : 0;
+}
+
+// ---------------------------------------------------- multi-pair products --
+// pair k: Q = q_aff[q_idx[k]] (G2 SoA over nq), P = p_aff[p_idx[k]] (G1 SoA over np_)
+// p_idx == -1 selects -g1.  One Miller loop per lane; product tree afterwards.
+__global__ void __launch_bounds__(KBLOCK) k_miller_pairs(size_t npairs, const uint32_t* __restrict__ q_aff, size_t nq,
+                                                        const int32_t* __restrict__ q_idx,
+                                                        const uint32_t* __restrict__ p_aff, size_t np_,
+                                                        const int32_t* __restrict__ p_idx,
+                                                        uint32_t* __restrict__ f_out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= npairs) return;
+  const aff_t<fp2_t> Q = soa_ld_g2(q_aff, nq, (size_t)q_idx[k]);
+  aff_t<fp_t> p;
+  const int32_t pi = p_idx[k];
+  if (pi < 0) { p.x = G1_GEN_X_M; p.y = G1_GEN_NEGY_M; }
+  else p = soa_ld_g1(p_aff, np_, (size_t)pi);
+  const g1_line_pre P = g1_prepare(p);
+  soa_st12(f_out, npairs, k, miller_loop_1(Q, P));
+}
+
+// out[j] = in[2j] * in[2j+1] (in[2j] alone if 2j+1 == m)
+__global__ void __launch_bounds__(KBLOCK) k_fp12_pair_product(size_t m, const uint32_t* __restrict__ in,
+                                                             uint32_t* __restrict__ out) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t half = (m + 1) / 2;
+  if (j >= half) return;
+  fp12_t a = soa_ld12(in, m, 2 * j);
+  if (2 * j + 1 < m) a = fp12_mul(a, soa_ld12(in, m, 2 * j + 1));
+  soa_st12(out, half, j, a);
+}
+
+// ---------------------------------------------------- aggregation kernels --
+// A chunk is a contiguous range [begin, end) of inputs belonging to one group.
+// Each workgroup sums one chunk: lanes stride over the chunk, then a tree
+// reduction of Jacobian partials staged in LDS.  The input is either
+// compressed points (level 1: decode + sum) or Jacobian SoA partials.
+struct agg_chunk { uint32_t begin, end; };
+
+template <class F> struct pt_traits;
+template <> struct pt_traits<fp_t> {
+  static constexpr int BYTES = 48;
+  __device__ static int decode(aff_t<fp_t>& a, const uint8_t* b) { return g1_decompress(a, b); }
+};
+template <> struct pt_traits<fp2_t> {
+  static constexpr int BYTES = 96;
+  __device__ static int decode(aff_t<fp2_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
+};
+
+template <class F, bool LEVEL1>
+__global__ void __launch_bounds__(KBLOCK) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
+                                                      const uint8_t* __restrict__ in_bytes,
+                                                      const uint32_t* __restrict__ in_jac, size_t n_in,
+                                                      const uint8_t* __restrict__ in_bad,
+                                                      uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad) {
+  constexpr int NW = sizeof(jac_t<F>) / 4;
+  __shared__ uint32_t lds[KBLOCK * NW];
+  __shared__ int bad_any;
+  const size_t c = blockIdx.x;
+  if (c >= nchunks) return;
+  const agg_chunk ch = chunks[c];
+  if (threadIdx.x == 0) bad_any = 0;
+  __syncthreads();
+  jac_t<F> acc = jac_infinity<F>();
+  bool bad = false;
+  for (uint32_t e = ch.begin + threadIdx.x; e < ch.end; e += blockDim.x) {
+    if (LEVEL1) {
+      uint8_t b[pt_traits<F>::BYTES];
+      ld_bytes(b, in_bytes + (size_t)pt_traits<F>::BYTES * e, pt_traits<F>::BYTES);
+      aff_t<F> a;
+      const int s = pt_traits<F>::decode(a, b);
+      if (s == PT_BAD) bad = true;
+      else if (s == PT_OK) acc = jac_add_aff(acc, a);
+    } else {
+      if (in_bad[e]) bad = true;
+      acc = jac_add(acc, soa_jac<F>::ld(in_jac, n_in, e));
+    }
+  }
+  if (bad) bad_any = 1;
+  // tree reduction through LDS (lane-major words: conflict-free stride-1 access)
+  uint32_t* mine = lds;
+  for (int s = KBLOCK / 2; s > 0; s >>= 1) {
+    __syncthreads();
+    if (threadIdx.x >= s && threadIdx.x < 2 * s) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(&acc);
+      for (int w = 0; w < NW; ++w) mine[w * KBLOCK + (threadIdx.x - s)] = src[w];
+    }
+    __syncthreads();
+    if (threadIdx.x < s) {
+      jac_t<F> o;
+      uint32_t* dst = reinterpret_cast<uint32_t*>(&o);
+      for (int w = 0; w < NW; ++w) dst[w] = mine[w * KBLOCK + threadIdx.x];
+      acc = jac_add(acc, o);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    soa_jac<F>::st(out_jac, nchunks, c, acc);
+    out_bad[c] = (uint8_t)bad_any;
+  }
+}
+
+// per group: Jacobian sum -> compressed bytes + status
+template <class F>
+__global__ void __launch_bounds__(KBLOCK) k_agg_compress(size_t ng, const uint32_t* __restrict__ jac,
+                                                        const uint8_t* __restrict__ bad,
+                                                        uint8_t* __restrict__ out, int32_t* __restrict__ status) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  if (bad[g]) { status[g] = BLS381_EINVAL_POINT; return; }
+  const jac_t<F> p = soa_jac<F>::ld(jac, ng, g);
+  uint8_t b[pt_traits<F>::BYTES];
+  if constexpr (pt_traits<F>::BYTES == 48) g1_compress(b, p);
+  else g2_compress(b, p);
+  for (int k = 0; k < pt_traits<F>::BYTES; ++k) out[(size_t)pt_traits<F>::BYTES * g + k] = b[k];
+  status[g] = 0;
+}
+
+// per group: Jacobian G1 sum -> affine + status (OK / INF / BAD incl. subgroup)
+__global__ void __launch_bounds__(KBLOCK) k_agg_g1_affine(size_t ng, const uint32_t* __restrict__ jac,
+                                                         const uint8_t* __restrict__ bad,
+                                                         uint32_t* __restrict__ out_aff, uint8_t* __restrict__ st) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  if (bad[g]) { st[g] = ST_BAD; return; }
+  aff_t<fp_t> a;
+  if (!jac_to_aff(a, soa_jac<fp_t>::ld(jac, ng, g))) { st[g] = ST_INF; return; }
+  if (!g1_in_subgroup(a)) { st[g] = ST_BAD; return; }
+  soa_st_g1(out_aff, ng, g, a);
+  st[g] = ST_OK;
+}
+
+// ------------------------------------------------------- sign / privtopub --
+__device__ __forceinline__ void scalar_limbs_from_be32(uint32_t k[8], const uint8_t* b) {
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* p = b + 28 - 4 * i;
+    k[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+  }
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_sign(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                const uint8_t* __restrict__ sks, const uint8_t* __restrict__ doms,
+                                                uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t scratch[BLS381_MSG_MAX + 9];
+  uint8_t dom[8];
+  ld_bytes(dom, doms + 8 * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  aff_t<fp2_t> h;
+  uint8_t sig[96];
+  if (!jac_to_aff(h, g2_mul_cofactor(c))) {
+    g2_compress(sig, jac_infinity<fp2_t>());
+  } else {
+    uint32_t k[8];
+    scalar_limbs_from_be32(k, sks + 32 * i);
+    g2_compress(sig, jac_mul_limbs(h, k, 256));
+  }
+  for (int b = 0; b < 96; ++b) out[96 * i + b] = sig[b];
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_privtopub(size_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t k[8];
+  scalar_limbs_from_be32(k, sks + 32 * i);
+  aff_t<fp_t> g; g.x = G1_GEN_X_M; g.y = G1_GEN_Y_M;
+  uint8_t pk[48];
+  g1_compress(pk, jac_mul_limbs(g, k, 256));
+  for (int b = 0; b < 48; ++b) out[48 * i + b] = pk[b];
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_hash_g2_out(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                       const uint8_t* __restrict__ doms,
+                                                       uint8_t* __restrict__ comp, uint8_t* __restrict__ affb) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t scratch[BLS381_MSG_MAX + 9];
+  uint8_t dom[8];
+  ld_bytes(dom, doms + 8 * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  aff_t<fp2_t> h;
+  uint8_t buf[96];
+  if (!jac_to_aff(h, g2_mul_cofactor(c))) {
+    g2_compress(buf, jac_infinity<fp2_t>());
+    for (int b = 0; b < 96; ++b) comp[96 * i + b] = buf[b];
+    for (int b = 0; b < 192; ++b) affb[192 * i + b] = 0;
+    return;
+  }
+  g2_compress_aff(buf, h);
+  for (int b = 0; b < 96; ++b) comp[96 * i + b] = buf[b];
+  fp_plain_to_be48(affb + 192 * i, fp_from_mont(h.x.c0));
+  fp_plain_to_be48(affb + 192 * i + 48, fp_from_mont(h.x.c1));
+  fp_plain_to_be48(affb + 192 * i + 96, fp_from_mont(h.y.c0));
+  fp_plain_to_be48(affb + 192 * i + 144, fp_from_mont(h.y.c1));
+}
+
+// ------------------------------------- py_ecc-exact projective hash_to_G2 --
+// Mirrors py_ecc optimized_bls12_381 homogeneous `double`/`add` and the
+// recursive `multiply` so the un-normalised triple
+// printed by test_generators/bls/main.py:66-72 is reproduced bit for bit.
+struct proj2 { fp2_t x, y, z; };
+
+__device__ inline proj2 pyecc_double(const proj2& p) {
+  const fp2_t W = fp2_mul_small(fp2_sqr(p.x), 3);
+  const fp2_t S = fp2_mul(p.y, p.z);
+  const fp2_t B = fp2_mul(fp2_mul(p.x, p.y), S);
+  const fp2_t H = fp2_sub(fp2_sqr(W), fp2_mul_small(B, 8));
+  const fp2_t S2 = fp2_sqr(S);
+  proj2 r;
+  r.x = fp2_mul_small(fp2_mul(H, S), 2);
+  r.y = fp2_sub(fp2_mul(W, fp2_sub(fp2_mul_small(B, 4), H)), fp2_mul_small(fp2_mul(fp2_sqr(p.y), S2), 8));
+  r.z = fp2_mul_small(fp2_mul(S, S2), 8);
+  return r;
+}
+
+__device__ inline proj2 pyecc_add(const proj2& p1, const proj2& p2) {
+  if (fp2_is_zero(p1.z) || fp2_is_zero(p2.z)) return fp2_is_zero(p2.z) ? p1 : p2;
+  const fp2_t U1 = fp2_mul(p2.y, p1.z);
+  const fp2_t U2 = fp2_mul(p1.y, p2.z);
+  const fp2_t V1 = fp2_mul(p2.x, p1.z);
+  const fp2_t V2 = fp2_mul(p1.x, p2.z);
+  if (fp2_eq(V1, V2) && fp2_eq(U1, U2)) return pyecc_double(p1);
+  if (fp2_eq(V1, V2)) { proj2 r; r.x = fp2_one(); r.y = fp2_one(); r.z = fp2_zero(); return r; }
+  const fp2_t U = fp2_sub(U1, U2);
+  const fp2_t V = fp2_sub(V1, V2);
+  const fp2_t V_sq = fp2_sqr(V);
+  const fp2_t V_sq_V2 = fp2_mul(V_sq, V2);
+  const fp2_t V_cu = fp2_mul(V, V_sq);
+  const fp2_t W = fp2_mul(p1.z, p2.z);
+  const fp2_t A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(U), W), V_cu), fp2_mul_small(V_sq_V2, 2));
+  proj2 r;
+  r.x = fp2_mul(V, A);
+  r.y = fp2_sub(fp2_mul(U, fp2_sub(V_sq_V2, A)), fp2_mul(V_cu, U2));
+  r.z = fp2_mul(V_cu, W);
+  return r;
+}
+
+// scratch: per item H2_BITS proj2 slots (SoA over n * H2_BITS entries, 6 Fp each)
+__global__ void __launch_bounds__(64) k_hash_g2_pyecc(size_t n, const uint8_t* __restrict__ msgs,
+                                                     const uint8_t* __restrict__ doms,
+                                                     uint32_t* __restrict__ scratch, uint8_t* __restrict__ out288) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint8_t sc[41];
+  uint8_t dom[8];
+  ld_bytes(dom, doms + 8 * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + 32 * i, 32, dom, sc);
+  const size_t ns = n * (size_t)H2_BITS;
+  auto slot = [&](int b) { return i * (size_t)H2_BITS + b; };
+  proj2 cur;
+  cur.x = c.x; cur.y = c.y; cur.z = fp2_one();
+  // doublings P_b = double^b(P) for b < top, stored; P_top is the accumulator start
+  for (int b = 0; b < H2_BITS - 1; ++b) {
+    const size_t s = slot(b);
+    soa_st2(scratch, ns, s, 0, cur.x); soa_st2(scratch, ns, s, 2, cur.y); soa_st2(scratch, ns, s, 4, cur.z);
+    cur = pyecc_double(cur);
+  }
+  proj2 acc = cur;
+  for (int b = H2_BITS - 2; b >= 0; --b) {
+    if ((H2_LIMBS[b >> 5] >> (b & 31)) & 1u) {
+      const size_t s = slot(b);
+      proj2 pb;
+      pb.x = soa_ld2(scratch, ns, s, 0); pb.y = soa_ld2(scratch, ns, s, 2); pb.z = soa_ld2(scratch, ns, s, 4);
+      acc = pyecc_add(acc, pb);
+    }
+  }
+  uint8_t* o = out288 + 288 * i;
+  const fp2_t* cs[3] = {&acc.x, &acc.y, &acc.z};
+  for (int k = 0; k < 3; ++k) {
+    fp_plain_to_be48(o + 96 * k, fp_from_mont(cs[k]->c0));
+    fp_plain_to_be48(o + 96 * k + 48, fp_from_mont(cs[k]->c1));
+  }
+}
+
+// -------------------------------------------------------- Fp12 byte codec --
+__global__ void k_fp12_to_bytes(const uint32_t* __restrict__ f, size_t n, size_t i, uint8_t* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const fp12_t a = soa_ld12(f, n, i);
+  const fp2_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int k = 0; k < 6; ++k) {
+    fp_plain_to_be48(out + 96 * k, fp_from_mont(cs[k]->c0));
+    fp_plain_to_be48(out + 96 * k + 48, fp_from_mont(cs[k]->c1));
+  }
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_fp12_from_bytes(size_t n, const uint8_t* __restrict__ in, uint32_t* __restrict__ f) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  fp12_t a;
+  fp2_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int k = 0; k < 6; ++k) {
+    cs[k]->c0 = fp_to_mont(fp_plain_from_be48(in + 576 * i + 96 * k));
+    cs[k]->c1 = fp_to_mont(fp_plain_from_be48(in + 576 * i + 96 * k + 48));
+  }
+  soa_st12(f, n, i, a);
+}
+
+}  // namespace bls381

@@ -1,0 +1,190 @@
+// Host unit-test build of the device arithmetic headers -- TEST INFRASTRUCTURE.
+//
+// g++ compiles the exact headers the gfx950 kernels use so that, in a container
+// with no GPU, every layer (Fp ... Fp12, codecs, subgroup checks, hash_to_G2,
+// Miller loop, final exponentiation) can be checked against oracle/ by
+// tests/test_host_arith.py.  This library is loaded only by tests; it is not a
+// fallback and the product library (libbls381.so) never links it.
+//
+// Byte conventions (all big-endian, plain / non-Montgomery values):
+//   Fp 48 B;  Fp2 96 B = re || im;  Fp12 576 B = a0,a1,a2,b0,b1,b2 (each Fp2)
+//   G1 affine 96 B = x || y;  G2 affine 192 B = x || y (each Fp2)
+#include <cstring>
+
+#include "bls381_hash.hpp"
+#include "bls381_pairing.hpp"
+
+using namespace bls381;
+
+namespace {
+fp_t ld(const uint8_t* p) { return fp_to_mont(fp_plain_from_be48(p)); }
+void st(uint8_t* p, const fp_t& a) { fp_plain_to_be48(p, fp_from_mont(a)); }
+fp2_t ld2(const uint8_t* p) { fp2_t r; r.c0 = ld(p); r.c1 = ld(p + 48); return r; }
+void st2(uint8_t* p, const fp2_t& a) { st(p, a.c0); st(p + 48, a.c1); }
+fp12_t ld12(const uint8_t* p) {
+  fp12_t r;
+  r.c0.c0 = ld2(p); r.c0.c1 = ld2(p + 96); r.c0.c2 = ld2(p + 192);
+  r.c1.c0 = ld2(p + 288); r.c1.c1 = ld2(p + 384); r.c1.c2 = ld2(p + 480);
+  return r;
+}
+void st12(uint8_t* p, const fp12_t& a) {
+  st2(p, a.c0.c0); st2(p + 96, a.c0.c1); st2(p + 192, a.c0.c2);
+  st2(p + 288, a.c1.c0); st2(p + 384, a.c1.c1); st2(p + 480, a.c1.c2);
+}
+aff_t<fp_t> ldg1(const uint8_t* p) { aff_t<fp_t> a; a.x = ld(p); a.y = ld(p + 48); return a; }
+aff_t<fp2_t> ldg2(const uint8_t* p) { aff_t<fp2_t> a; a.x = ld2(p); a.y = ld2(p + 96); return a; }
+}  // namespace
+
+extern "C" {
+
+void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_mul(ld(a), ld(b))); }
+void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_add(ld(a), ld(b))); }
+void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_sub(ld(a), ld(b))); }
+void hc_fp_half(const uint8_t* a, uint8_t* o) { st(o, fp_half(ld(a))); }
+void hc_fp_inv(const uint8_t* a, uint8_t* o) { st(o, fp_inv(ld(a))); }
+int hc_fp_sqrt(const uint8_t* a, uint8_t* o) {
+  fp_t r;
+  const bool ok = fp_sqrt(r, ld(a));
+  st(o, r);
+  return ok;
+}
+// raw Montgomery multiply on plain limbs (checks fp_mul's bound handling directly)
+void hc_fp_mont_mul_raw(const uint8_t* a, const uint8_t* b, uint8_t* o) {
+  fp_plain_to_be48(o, fp_mul(fp_plain_from_be48(a), fp_plain_from_be48(b)));
+}
+
+void hc_fp2_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st2(o, fp2_mul(ld2(a), ld2(b))); }
+void hc_fp2_sqr(const uint8_t* a, uint8_t* o) { st2(o, fp2_sqr(ld2(a))); }
+void hc_fp2_inv(const uint8_t* a, uint8_t* o) { st2(o, fp2_inv(ld2(a))); }
+int hc_fp2_sqrt_select(const uint8_t* a, uint8_t* o) {
+  fp2_t r;
+  if (!fp2_sqrt(r, ld2(a))) return 0;
+  st2(o, g2_select_root(r));
+  return 1;
+}
+
+void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st12(o, fp12_mul(ld12(a), ld12(b))); }
+void hc_fp12_sqr(const uint8_t* a, uint8_t* o) { st12(o, fp12_sqr(ld12(a))); }
+void hc_fp12_inv(const uint8_t* a, uint8_t* o) { st12(o, fp12_inv(ld12(a))); }
+void hc_fp12_frob(const uint8_t* a, int p, uint8_t* o) { st12(o, fp12_frob(ld12(a), p)); }
+void hc_fp12_cyc_sqr(const uint8_t* a, uint8_t* o) { st12(o, fp12_cyclotomic_sqr(ld12(a))); }
+void hc_fp12_mul_by_line(const uint8_t* f, const uint8_t* c0, const uint8_t* c1, const uint8_t* c2, uint8_t* o) {
+  st12(o, fp12_mul_by_line(ld12(f), ld2(c0), ld2(c1), ld2(c2)));
+}
+void hc_final_exp(const uint8_t* a, uint8_t* o) { st12(o, final_exp(ld12(a))); }
+
+int hc_g1_decompress(const uint8_t* b48, uint8_t* aff96) {
+  aff_t<fp_t> a;
+  const int s = g1_decompress(a, b48);
+  if (s == PT_OK) { st(aff96, a.x); st(aff96 + 48, a.y); }
+  return s;
+}
+int hc_g2_decompress(const uint8_t* b96, uint8_t* aff192) {
+  aff_t<fp2_t> a;
+  const int s = g2_decompress(a, b96);
+  if (s == PT_OK) { st2(aff192, a.x); st2(aff192 + 96, a.y); }
+  return s;
+}
+void hc_g1_compress_aff(const uint8_t* aff96, uint8_t* b48) { g1_compress(b48, jac_from_aff(ldg1(aff96))); }
+void hc_g2_compress_aff(const uint8_t* aff192, uint8_t* b96) { g2_compress_aff(b96, ldg2(aff192)); }
+int hc_g1_in_subgroup(const uint8_t* aff96) { return g1_in_subgroup(ldg1(aff96)); }
+int hc_g2_in_subgroup(const uint8_t* aff192) { return g2_in_subgroup(ldg2(aff192)); }
+
+int hc_hash_to_g2(const uint8_t* msg, uint32_t mlen, const uint8_t* dom8, uint8_t* aff192, uint8_t* comp96) {
+  uint8_t scratch[256 + 9];
+  if (mlen > 256) return -1;
+  aff_t<fp2_t> c;
+  const int trials = hash_to_g2_candidate(c, msg, mlen, dom8, scratch);
+  aff_t<fp2_t> h;
+  if (!jac_to_aff(h, g2_mul_cofactor(c))) return -2;
+  st2(aff192, h.x); st2(aff192 + 96, h.y);
+  g2_compress_aff(comp96, h);
+  return trials;
+}
+void hc_sha256(const uint8_t* msg, uint32_t len, uint8_t* out32) {
+  uint32_t d[8];
+  sha256(d, msg, len);
+  for (int i = 0; i < 8; ++i) {
+    out32[4 * i] = (uint8_t)(d[i] >> 24); out32[4 * i + 1] = (uint8_t)(d[i] >> 16);
+    out32[4 * i + 2] = (uint8_t)(d[i] >> 8); out32[4 * i + 3] = (uint8_t)d[i];
+  }
+}
+
+// Miller loop of n <= 4 pairs (G2 affine 192 B each, G1 affine 96 B each)
+int hc_miller_loop(int n, const uint8_t* q192, const uint8_t* p96, uint8_t* o576) {
+  aff_t<fp2_t> Q[4];
+  g1_line_pre P[4];
+  if (n < 1 || n > 4) return -1;
+  for (int k = 0; k < n; ++k) { Q[k] = ldg2(q192 + 192 * k); P[k] = g1_prepare(ldg1(p96 + 96 * k)); }
+  fp12_t f;
+  switch (n) {
+    case 1: f = miller_loop_n<1>(Q, P); break;
+    case 2: f = miller_loop_n<2>(Q, P); break;
+    case 3: f = miller_loop_n<3>(Q, P); break;
+    default: f = miller_loop_n<4>(Q, P); break;
+  }
+  st12(o576, f);
+  return 0;
+}
+
+// G1 / G2 scalar multiplication with the same curve code (fixture helpers)
+void hc_g1_mul(const uint8_t* aff96, const uint32_t* k_limbs, int nbits, uint8_t* b48) {
+  g1_compress(b48, jac_mul_limbs(ldg1(aff96), k_limbs, nbits));
+}
+void hc_g2_mul(const uint8_t* aff192, const uint32_t* k_limbs, int nbits, uint8_t* b96) {
+  g2_compress(b96, jac_mul_limbs(ldg2(aff192), k_limbs, nbits));
+}
+
+#if defined(BLS_COUNT_OPS)
+// Per-stage Fp-multiplication counts of one bls_verify exactly as the gfx950
+// kernels of bls381_capi.hip stage it (decode_g1 + subgroup, decode_g2 +
+// subgroup, hash_to_g2, miller_loop_2, final_exp).  out[5] receives the counts.
+int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig96, const uint8_t* dom8,
+                           uint64_t* out) {
+  aff_t<fp_t> P;
+  aff_t<fp2_t> S, H;
+  g_fp_mul_count = 0;
+  int sp = g1_decompress(P, pk48);
+  if (sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
+  out[0] = g_fp_mul_count;
+  g_fp_mul_count = 0;
+  int ss = g2_decompress(S, sig96);
+  if (ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
+  out[1] = g_fp_mul_count;
+  g_fp_mul_count = 0;
+  uint8_t scratch[41];
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msg32, 32, dom8, scratch);
+  jac_to_aff(H, g2_mul_cofactor(c));
+  out[2] = g_fp_mul_count;
+  if (sp != PT_OK || ss != PT_OK) { out[3] = out[4] = 0; return -1; }
+  g_fp_mul_count = 0;
+  aff_t<fp2_t> Q[2] = {S, H};
+  aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+  g1_line_pre Pp[2] = {g1_prepare(ng), g1_prepare(P)};
+  const fp12_t f = miller_loop_n<2>(Q, Pp);
+  out[3] = g_fp_mul_count;
+  g_fp_mul_count = 0;
+  const bool ok = fp12_is_one(final_exp(f));
+  out[4] = g_fp_mul_count;
+  return ok ? 1 : 0;
+}
+
+// Fp multiplications of one committee aggregation of n pubkeys (decode + adds)
+int hc_count_aggregate(size_t n, const uint8_t* pks, uint64_t* out) {
+  g_fp_mul_count = 0;
+  jac_t<fp_t> acc = jac_infinity<fp_t>();
+  for (size_t i = 0; i < n; ++i) {
+    aff_t<fp_t> a;
+    const int s = g1_decompress(a, pks + 48 * i);
+    if (s == PT_BAD) return -1;
+    if (s == PT_OK) acc = jac_add_aff(acc, a);
+  }
+  uint8_t b[48];
+  g1_compress(b, acc);
+  *out = g_fp_mul_count;
+  return 0;
+}
+#endif
+
+}  // extern "C"

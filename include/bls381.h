@@ -1,0 +1,136 @@
+/*
+ * bls381.h -- C ABI of the MI355X (gfx950) BLS12-381 engine.
+ *
+ * Drop-in boundary for the reference's BLS path: every entry point below is
+ * what `test_libs/pyspec/eth2spec/utils/bls.py` (reference) would bind through
+ * ctypes in place of `from py_ecc import bls` (bls.py:1).  The Python mirror of
+ * that module is consensus-specs_amd/bls381_amd/bls.py; the binding a
+ * maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; the caller owns every buffer.
+ *   - Pubkeys are 48-byte compressed G1, signatures 96-byte compressed G2
+ *     (specs/bls_signature.md:36-64).  Messages are `msg_len` bytes (the spec's
+ *     message_hash is Bytes32; py_ecc hashes any length, so 0..MSG_MAX is accepted).
+ *   - `dom8` is the 8-byte serialisation of the spec's uint64 `domain`
+ *     (hash_to_G2, bls_signature.md:76-77).  The int -> bytes step is done by
+ *     the caller so the byte order has one switch.
+ *   - Return codes: >= 0 success (verdicts 1/0), < 0 error (BLS381_E*).
+ *   - Host-pointer entry points copy to/from the device internally.  The
+ *     `_device` variants take device pointers and a hipStream_t (as void*).
+ *   - There is no CPU fallback: without a usable gfx950 device every call
+ *     returns BLS381_ENODEV.
+ */
+#ifndef BLS381_H
+#define BLS381_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BLS381_OK 0
+#define BLS381_EINVAL_POINT (-1) /* an input point encoding is invalid (aggregate raises ValueError) */
+#define BLS381_EARG (-2)         /* bad argument (NULL, length) */
+#define BLS381_ENODEV (-3)       /* no HIP device / kernels not loadable */
+#define BLS381_EHIP (-4)         /* HIP runtime error */
+#define BLS381_MSG_MAX 256
+
+/* ---- runtime ----------------------------------------------------------- */
+/* Number of visible HIP devices (0 if none). */
+int bls381_device_count(void);
+/* Select the device used by subsequent calls from this thread and create its
+ * context (stream, workspace).  Idempotent. */
+int bls381_init(int device);
+void bls381_shutdown(void);
+/* Last HIP error string of this thread (static storage). */
+const char* bls381_last_error(void);
+/* Kernel-time accounting (HIP events on the launch stream) for bench.py. */
+int bls381_profile_enable(int on);
+int bls381_profile_read(char* json_out, size_t cap);
+
+/* ---- eth2spec.utils.bls drop-ins (reference bls.py:24-46) -------------- */
+
+/* bls_verify (bls.py:24-26; bls_signature.md:131-137).  1 = valid, 0 = invalid
+ * (including undecodable inputs, as py_ecc's except-clause returns False). */
+int bls381_verify(const uint8_t pk[48], const uint8_t* msg, size_t msg_len,
+                  const uint8_t sig[96], const uint8_t dom8[8]);
+
+/* bls_verify_multiple (bls.py:29-31; bls_signature.md:139-146).  n pubkeys and
+ * n messages of msg_len bytes each; pubkeys sharing a message are aggregated
+ * first (py_ecc grouping) and one final exponentiation decides the call. */
+int bls381_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len,
+                           const uint8_t sig[96], const uint8_t dom8[8]);
+
+/* bls_aggregate_pubkeys (bls.py:34-36): sum of n G1 points; n == 0 -> infinity.
+ * Returns BLS381_EINVAL_POINT if any input does not decode. */
+int bls381_aggregate_pubkeys(size_t n, const uint8_t* pks, uint8_t out[48]);
+
+/* bls_aggregate_signatures (bls.py:39-41): sum of n G2 points. */
+int bls381_aggregate_signatures(size_t n, const uint8_t* sigs, uint8_t out[96]);
+
+/* bls_sign (bls.py:44-46): [sk] hash_to_G2(msg, domain); sk 32-byte big-endian. */
+int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const uint8_t dom8[8],
+                uint8_t out[96]);
+
+/* py_ecc bls.privtopub (test_generators/bls/main.py:114; helpers/keys.py:5). */
+int bls381_privtopub(const uint8_t sk[32], uint8_t out[48]);
+
+/* Batched sign / privtopub over n items (32-byte messages, 32-byte big-endian
+ * secret keys, per-item dom8) -- used to build synthetic verify batches. */
+int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const uint8_t* dom8s, uint8_t* out96);
+int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48);
+
+/* hash_to_G2 (bls_signature.md:74-87; main.py:71,84): compressed (96 B) and
+ * normalised affine x_re,x_im,y_re,y_im (4 x 48 B big-endian).  Either output may be NULL. */
+int bls381_hash_to_g2(const uint8_t* msg, size_t msg_len, const uint8_t dom8[8],
+                      uint8_t out_compressed[96], uint8_t out_affine[192]);
+
+/* py_ecc's un-normalised projective triple for hash_to_G2 (main.py:56-72,
+ * msg_hash_g2_uncompressed vectors): X,Y,Z each (re, im), 6 x 48 B big-endian.
+ * n messages of 32 bytes with per-message dom8. */
+int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const uint8_t* dom8s,
+                                       uint8_t* out288);
+
+/* ---- batched entry points (the throughput path) ------------------------ */
+
+/* n independent bls_verify calls: verdicts_out[i] = 1/0. */
+int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
+                        const uint8_t* dom8s, uint8_t* verdicts_out);
+
+/* Device-resident variant: all pointers are device memory, stream = hipStream_t.
+ * `workspace` must hold bls381_verify_batch_workspace_size(n) bytes. */
+size_t bls381_verify_batch_workspace_size(size_t n);
+int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32,
+                               const uint8_t* d_sigs, const uint8_t* d_dom8s, uint8_t* d_verdicts,
+                               void* d_workspace, void* stream);
+
+/* Committee aggregation (config C3/C4): n_groups groups, group g = pubkeys
+ * [offsets[g], offsets[g+1]).  out48 receives n_groups compressed sums; status[g]
+ * is 0, or BLS381_EINVAL_POINT when a member does not decode. */
+int bls381_aggregate_pubkeys_batch(size_t n_groups, const uint32_t* offsets, const uint8_t* pks,
+                                   uint8_t* out48, int32_t* status);
+size_t bls381_aggregate_pubkeys_batch_workspace_size(size_t n_groups, size_t n_pks);
+/* h_offsets is a HOST array (n_groups + 1 entries): the grouping plan is built on the host. */
+int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_offsets, size_t n_pks,
+                                          const uint8_t* d_pks, uint8_t* d_out48, int32_t* d_status,
+                                          void* d_workspace, void* stream);
+
+/* ---- multi-GPU partial products --------------------------- */
+/* Miller-loop product of one shard of a bls_verify_multiple call: pairs
+ * (hash_to_G2(msg_g), group_pubkey_g) for the messages in this shard, plus
+ * (sig, -g1) when include_sig != 0.  out576 = Fp12 in the engine's tower
+ * (a0..b2, each re||im, 48-byte big-endian).  Returns 0, or 1 when an input
+ * fails to decode / fails a subgroup check (the call's verdict is then False). */
+int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len,
+                          const uint8_t sig[96], int include_sig, const uint8_t dom8[8],
+                          uint8_t out576[576]);
+/* Multiply k partial products and run one final exponentiation: 1 / 0. */
+int bls381_final_verify(size_t k, const uint8_t* parts576);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BLS381_H */

@@ -1,0 +1,33 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "consensus-specs_amd"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) device")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    d = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(d, "bls_vectors.json")) as f:
+        vec = json.load(f)
+    with open(os.path.join(d, "bls_golden_batches.json")) as f:
+        gb = json.load(f)
+    return vec, gb
+
+
+@pytest.fixture(scope="session")
+def native():
+    """The HIP engine; GPU tests fail loudly if it is not loadable."""
+    from bls381_amd import _native
+    _native.init(0)
+    return _native

@@ -1,0 +1,196 @@
+"""Host (g++) build of the device arithmetic headers vs the oracle / model.
+
+The same headers are compiled for gfx950 by hipcc; this suite checks every
+layer of them in a container with no GPU.  libbls381_hostcheck.so is test
+infrastructure (consensus-specs_amd/csrc/host_check.cpp), never the product.
+"""
+import ctypes
+import hashlib
+import os
+import random
+
+import pytest
+
+import bls_oracle as O
+import tower_model as M
+
+q = O.q
+
+
+@pytest.fixture(scope="module")
+def L():
+    import build_native
+    return ctypes.CDLL(build_native.build_hostcheck())
+
+
+def b48(x): return x.to_bytes(48, "big")
+def i48(b): return int.from_bytes(b, "big")
+def b96(a): return b48(a[0]) + b48(a[1])
+def i96(b): return (i48(b[:48]), i48(b[48:96]))
+def b576(f): return b"".join(b96(c) for c in f)
+def i576(b): return tuple(i96(b[96 * i:96 * i + 96]) for i in range(6))
+
+
+def test_fp_ops(L):
+    rng = random.Random(5)
+    buf = ctypes.create_string_buffer(48)
+    edge = [(q - 1, q - 1), (0, q - 1), (1, 1), (q - 1, 1), (0, 0), (2 ** 256, q - 2)]
+    for i in range(400):
+        a, b = edge[i] if i < len(edge) else (rng.randrange(q), rng.randrange(q))
+        L.hc_fp_mul(b48(a), b48(b), buf); assert i48(buf.raw) == a * b % q
+        L.hc_fp_add(b48(a), b48(b), buf); assert i48(buf.raw) == (a + b) % q
+        L.hc_fp_sub(b48(a), b48(b), buf); assert i48(buf.raw) == (a - b) % q
+        L.hc_fp_half(b48(a), buf); assert i48(buf.raw) * 2 % q == a
+    # raw Montgomery product stays < q for all inputs < q
+    R = 1 << 384
+    Rinv = pow(R, -1, q)
+    for _ in range(100):
+        a, b = rng.randrange(q), rng.randrange(q)
+        L.hc_fp_mont_mul_raw(b48(a), b48(b), buf)
+        assert i48(buf.raw) == a * b * Rinv % q
+
+
+def test_fp_inv_sqrt(L):
+    rng = random.Random(6)
+    buf = ctypes.create_string_buffer(48)
+    for _ in range(10):
+        a = rng.randrange(1, q)
+        L.hc_fp_inv(b48(a), buf); assert i48(buf.raw) * a % q == 1
+        s = L.hc_fp_sqrt(b48(a), buf)
+        r = i48(buf.raw)
+        assert bool(s) == (pow(a, (q - 1) // 2, q) == 1)
+        if s:
+            assert r * r % q == a
+
+
+def test_fp2(L):
+    rng = random.Random(7)
+    buf = ctypes.create_string_buffer(96)
+    for i in range(60):
+        a, b = (rng.randrange(q), rng.randrange(q)), (rng.randrange(q), rng.randrange(q))
+        L.hc_fp2_mul(b96(a), b96(b), buf); assert i96(buf.raw) == M.mul2(a, b)
+        L.hc_fp2_sqr(b96(a), buf); assert i96(buf.raw) == M.mul2(a, a)
+        L.hc_fp2_inv(b96(a), buf); assert i96(buf.raw) == M.inv2(a)
+    for i in range(60):
+        v = (rng.randrange(q), rng.randrange(q)) if i % 4 else (rng.randrange(q), 0)
+        if i == 1:
+            v = (0, rng.randrange(q))
+        s = L.hc_fp2_sqrt_select(b96(v), buf)
+        e = O.modular_squareroot(v)
+        assert (e is None) == (s == 0)
+        if e is not None:
+            assert i96(buf.raw) == e
+
+
+def test_fp12(L):
+    rng = random.Random(8)
+    buf = ctypes.create_string_buffer(576)
+    r2 = lambda: (rng.randrange(q), rng.randrange(q))
+    f = tuple(r2() for _ in range(6))
+    g = tuple(r2() for _ in range(6))
+    L.hc_fp12_mul(b576(f), b576(g), buf); assert i576(buf.raw) == M.mul12(f, g)
+    L.hc_fp12_sqr(b576(f), buf); assert i576(buf.raw) == M.mul12(f, f)
+    L.hc_fp12_inv(b576(f), buf); assert i576(buf.raw) == M.inv12(f)
+    for p in (1, 2, 3):
+        L.hc_fp12_frob(b576(f), p, buf); assert i576(buf.raw) == M.frob12(f, p)
+    t = M.mul12(M.conj12(f), M.inv12(f))
+    t = M.mul12(M.frob12(t, 2), t)
+    L.hc_fp12_cyc_sqr(b576(t), buf); assert i576(buf.raw) == M.mul12(t, t)
+    c = [r2() for _ in range(3)]
+    L.hc_fp12_mul_by_line(b576(f), b96(c[0]), b96(c[1]), b96(c[2]), buf)
+    assert i576(buf.raw) == M.mul12(f, (c[0], c[1], M.ZERO2, M.ZERO2, c[2], M.ZERO2))
+    L.hc_final_exp(b576(f), buf); assert i576(buf.raw) == M.final_exp(f)
+
+
+def test_codecs_and_subgroups(L, golden):
+    vec, gb = golden
+    buf = ctypes.create_string_buffer(192)
+    for c in vec["priv_to_pub"]:
+        pk = bytes.fromhex(c["output"][2:])
+        assert L.hc_g1_decompress(pk, buf) == 0
+        assert O.pubkey_to_G1(pk) == (i48(buf.raw[:48]), i48(buf.raw[48:96]), 1)
+        out = ctypes.create_string_buffer(48)
+        L.hc_g1_compress_aff(buf.raw[:96], out)
+        assert out.raw == pk
+        assert L.hc_g1_in_subgroup(buf.raw[:96]) == 1
+    for c in vec["sign_msg"][::5]:
+        sig = bytes.fromhex(c["output"][2:])
+        assert L.hc_g2_decompress(sig, buf) == 0
+        a = O.signature_to_G2(sig)
+        assert (i96(buf.raw[:96]), i96(buf.raw[96:192])) == (a[0], a[1])
+        out = ctypes.create_string_buffer(96)
+        L.hc_g2_compress_aff(buf.raw, out)
+        assert out.raw == sig
+        assert L.hc_g2_in_subgroup(buf.raw) == 1
+    for h in gb["invalid_g1"]:
+        assert L.hc_g1_decompress(bytes.fromhex(h), buf) == 2
+    for h in gb["invalid_g2"]:
+        assert L.hc_g2_decompress(bytes.fromhex(h), buf) == 2
+    assert L.hc_g1_decompress(bytes([0xC0]) + b"\x00" * 47, buf) == 1
+    assert L.hc_g2_decompress(bytes([0xC0]) + b"\x00" * 95, buf) == 1
+    s = M.sqrt_fp((5 ** 3 + 4) % q)
+    assert L.hc_g1_in_subgroup(b48(5) + b48(s)) == 0
+    x, y = M.map_candidate(b"\x11" * 32, b"\x00" * 8)
+    assert L.hc_g2_in_subgroup(b96(x) + b96(y)) == 0
+
+
+def test_sha256_any_length(L):
+    rng = random.Random(9)
+    out = ctypes.create_string_buffer(32)
+    for n in (0, 1, 41, 55, 56, 63, 64, 65, 119, 200, 256):
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        L.hc_sha256(m, n, out)
+        assert out.raw == hashlib.sha256(m).digest()
+
+
+def test_hash_to_g2_vectors(L, golden):
+    vec, gb = golden
+    aff = ctypes.create_string_buffer(192)
+    comp = ctypes.create_string_buffer(96)
+    for c in vec["msg_hash_g2_compressed"]:
+        m = bytes.fromhex(c["input"]["message"][2:])
+        d = int(c["input"]["domain"], 16).to_bytes(8, "big")
+        assert L.hc_hash_to_g2(m, 32, d, aff, comp) > 0
+        assert comp.raw.hex() == c["output"][0][2:] + c["output"][1][2:]
+    for c in gb["hash_to_g2"]:
+        m, d = bytes.fromhex(c["message"]), int(c["domain"]).to_bytes(8, "big")
+        assert L.hc_hash_to_g2(m, 32, d, aff, comp) == c["trials"]
+        assert comp.raw.hex() == c["compressed"]
+    m = b"variable length message"
+    assert L.hc_hash_to_g2(m, len(m), b"\x00" * 8, aff, comp) > 0
+    assert comp.raw == O.G2_to_signature(O.hash_to_G2(m, 0))
+
+
+def test_miller_loop_and_verify_equation(L):
+    rng = random.Random(10)
+    buf = ctypes.create_string_buffer(576)
+    fo = ctypes.create_string_buffer(576)
+    sk = rng.randrange(1, O.r)
+    msg, dom = bytes(range(32)), 9
+    pk = O.pubkey_to_G1(O.privtopub(sk))
+    sa = O.g2_affine(O.signature_to_G2(O.sign(msg, sk, dom)))
+    H = O.g2_affine(O.hash_to_G2(msg, dom))
+    ng = (O.g_x, (-O.g_y) % q)
+    Q = b96(sa[0]) + b96(sa[1]) + b96(H[0]) + b96(H[1])
+    P = b48(ng[0]) + b48(ng[1]) + b48(pk[0]) + b48(pk[1])
+    L.hc_miller_loop(2, Q, P, buf)
+    assert i576(buf.raw) == M.miller_loop_multi([(sa, ng), (H, (pk[0], pk[1]))])
+    L.hc_final_exp(buf.raw, fo)
+    assert i576(fo.raw) == M.ONE12
+    # wrong public key -> not one
+    pk2 = O.pubkey_to_G1(O.privtopub(sk + 1))
+    P2 = b48(ng[0]) + b48(ng[1]) + b48(pk2[0]) + b48(pk2[1])
+    L.hc_miller_loop(2, Q, P2, buf)
+    L.hc_final_exp(buf.raw, fo)
+    assert i576(fo.raw) != M.ONE12
+    # single-pair loop matches the model too
+    L.hc_miller_loop(1, Q[:192], P[:96], buf)
+    assert i576(buf.raw) == M.miller_loop_multi([(sa, ng)])
+
+
+def test_scalar_mul_fixture_helpers(L):
+    out = ctypes.create_string_buffer(48)
+    k = 0x263dbd792f5b1be47ed85f8938c0f29586af0d3ac7b977f21c278fe1462040e3
+    limbs = (ctypes.c_uint32 * 8)(*[(k >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
+    L.hc_g1_mul(b48(O.g_x) + b48(O.g_y), limbs, 256, out)
+    assert out.raw == O.privtopub(k)

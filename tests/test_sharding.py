@@ -1,0 +1,120 @@
+"""Multi-rank bls_verify_multiple protocol (bls381_amd.sharding) on CPU/gloo.
+
+World size 2, gloo backend, 127.0.0.1.  The per-rank partial product and the
+final exponentiation use the CPU model of the engine's tower
+(oracle/tower_model.py) in place of the GPU, so the partition / all-gather /
+single-final-exponentiation protocol is checked here; the GPU-side partials
+are checked by tests/test_gpu_parity.py::test_partial_products_combine.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def model_partial(pks, msgs, mlen, sig, include_sig, dom8):
+    import bls_oracle as O
+    import tower_model as M
+    pairs = []
+    n = len(pks) // 48
+    groups = {}
+    order = []
+    for i in range(n):
+        m = msgs[mlen * i:mlen * (i + 1)]
+        if m not in groups:
+            groups[m] = O.Z1
+            order.append(m)
+        groups[m] = O.pt_add(O.FqOps, groups[m], O.pubkey_to_G1(pks[48 * i:48 * (i + 1)]))
+    dom = int.from_bytes(dom8, "big")
+    for m in order:
+        if O.pt_is_inf(O.FqOps, groups[m]):
+            continue
+        pairs.append((O.g2_affine(O.hash_to_G2(m, dom)), O.pt_normalize(O.FqOps, groups[m])))
+    if include_sig:
+        s = O.signature_to_G2(sig)
+        if not O.pt_is_inf(O.Fq2Ops, s):
+            pairs.append((O.g2_affine(s), (O.g_x, (-O.g_y) % O.q)))
+    f = M.miller_loop_multi(pairs) if pairs else M.ONE12
+    return 0, b"".join(c[0].to_bytes(48, "big") + c[1].to_bytes(48, "big") for c in f)
+
+
+def model_final(parts):
+    import tower_model as M
+    f = M.ONE12
+    for k in range(len(parts) // 576):
+        p = parts[576 * k:576 * (k + 1)]
+        g = tuple((int.from_bytes(p[96 * i:96 * i + 48], "big"), int.from_bytes(p[96 * i + 48:96 * i + 96], "big"))
+                  for i in range(6))
+        f = M.mul12(f, g)
+    return M.final_exp(f) == M.ONE12
+
+
+def _worker(rank, world, port, case, q):
+    sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+    from bls381_amd import sharding
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
+    pks, msgs, sig, dom = case
+    v = sharding.sharded_verify_multiple(pks, msgs, sig, dom, rank=rank, world=world,
+                                         partial_fn=model_partial, final_fn=model_final)
+    q.put((rank, v))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(case, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    res = dict(q.get() for _ in range(world))
+    return res
+
+
+@pytest.fixture(scope="module")
+def case():
+    import bls_oracle as O
+    sks = [11, 22, 33, 44]
+    msgs = [b"\x01" * 32, b"\x02" * 32, b"\x01" * 32, b"\x03" * 32]
+    pks = [O.privtopub(k) for k in sks]
+    sig = O.aggregate_signatures([O.sign(m, k, 5) for m, k in zip(msgs, sks)])
+    return pks, msgs, sig, 5
+
+
+def test_partition_keeps_message_groups_on_one_rank():
+    from bls381_amd.sharding import partition_messages
+    msgs = [b"a", b"b", b"a", b"c", b"b", b"d"]
+    sh = partition_messages(msgs, 2)
+    assert sorted(sh[0] + sh[1]) == list(range(6))
+    for r in range(2):
+        for m in {msgs[i] for i in sh[r]}:
+            assert all(i in sh[r] for i in range(6) if msgs[i] == m)
+
+
+def test_sharded_verify_multiple_gloo_world2(case):
+    import bls_oracle as O
+    pks, msgs, sig, dom = case
+    assert O.verify_multiple(pks, msgs, sig, dom) is True
+    res = _run(case)
+    assert res == {0: True, 1: True}
+    bad = (pks[::-1], msgs, sig, dom)
+    res = _run(bad)
+    assert res == {0: False, 1: False}

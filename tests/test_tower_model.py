@@ -1,0 +1,62 @@
+"""oracle/tower_model.py (our device algorithms) vs oracle/bls_oracle.py (reference)."""
+import random
+
+import bls_oracle as O
+import tower_model as M
+
+q = O.q
+
+
+def _r2(rng):
+    return (rng.randrange(q), rng.randrange(q))
+
+
+def test_tower_is_isomorphic_to_pyecc_fq12():
+    rng = random.Random(1)
+    f = tuple(_r2(rng) for _ in range(6))
+    g = tuple(_r2(rng) for _ in range(6))
+    assert M.to_pyecc12(M.mul12(f, g)) == O.f12_mul(M.to_pyecc12(f), M.to_pyecc12(g))
+    assert M.to_pyecc12(M.frob12(f, 1)) == O.f12_pow(M.to_pyecc12(f), q)
+    assert M.mul12(M.inv12(f), f) == M.ONE12
+
+
+def test_cyclotomic_square_and_final_exp_chain():
+    rng = random.Random(2)
+    f = tuple(_r2(rng) for _ in range(6))
+    t = M.mul12(M.conj12(f), M.inv12(f))
+    t = M.mul12(M.frob12(t, 2), t)
+    assert M.cyclotomic_sqr(t) == M.mul12(t, t)
+    assert M.to_pyecc12(M.final_exp(f)) == O.f12_pow(M.to_pyecc12(f), 3 * (q ** 12 - 1) // O.r)
+
+
+def test_pairing_bilinear_and_relation_to_oracle():
+    rng = random.Random(3)
+    g1 = (O.g_x, O.g_y)
+    g2 = (O.G2_gen_x, O.G2_gen_y)
+    e = M.pairing(g2, g1)
+    a, b = rng.randrange(O.r), rng.randrange(O.r)
+    aP = O.pt_normalize(O.FqOps, O.pt_multiply(O.FqOps, O.G1, a))
+    bQ = O.pt_normalize(O.Fq2Ops, O.pt_multiply(O.Fq2Ops, O.G2, b))
+    assert M.pairing(bQ, aP) == M.pow12(e, a * b % O.r)
+    # ours = oracle^-3 (conjugation for x < 0, factor 3 in the hard part)
+    assert M.to_pyecc12(e) == O.f12_pow(O.pairing(O.G2, O.G1), (-3) % O.r)
+
+
+def test_hash_sqrt_subgroup_models():
+    rng = random.Random(4)
+    for i in range(60):
+        v = _r2(rng) if i % 4 else (rng.randrange(q), 0)
+        a, b = O.modular_squareroot(v), M.sqrt_fp2(v)
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert M.choose_root(b) == a
+    msg, dom = bytes(range(32)), 77
+    H = M.hash_to_g2_affine(msg, dom.to_bytes(8, "big"))
+    assert H == O.g2_affine(O.hash_to_G2(msg, dom))
+    assert M.g2_in_subgroup((H[0], H[1], M.ONE2))
+    x, y = M.map_candidate(msg, b"abcdefgh")
+    assert not M.g2_in_subgroup((x, y, M.ONE2))
+    pk = O.pt_normalize(O.FqOps, O.pubkey_to_G1(O.privtopub(99)))
+    assert M.g1_in_subgroup((pk[0], pk[1], 1))
+    s = M.sqrt_fp((5 ** 3 + 4) % q)
+    assert not M.g1_in_subgroup((5, s, 1))
