@@ -259,7 +259,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)",
+        "dtype": "u32 (381-bit Montgomery, 14x28-bit limbs in u32 words)",
         "data": "synthetic (random keys/messages, signatures made on device)",
         "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
                    "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world},

@@ -110,6 +110,7 @@ struct Bump {
   }
 };
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+constexpr size_t FPW = 4 * FP_LIMBS;   // bytes per Fp element in SoA buffers
 
 unsigned grid_for(size_t n, int block = KBLOCK) { return (unsigned)((n + block - 1) / block); }
 
@@ -145,15 +146,15 @@ struct VerifyWs {
   uint8_t *pk_st, *sig_st, *f_st;
 };
 size_t verify_ws_size(size_t n) {
-  return align256(24 * 4 * n) + align256(48 * 4 * n) * 2 + align256(144 * 4 * n) + 3 * align256(n) + 1024;
+  return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * n) + 3 * align256(n) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n) {
   Bump b(ws);
   VerifyWs w;
-  w.pk_aff = b.take<uint32_t>(24 * n);
-  w.sig_aff = b.take<uint32_t>(48 * n);
-  w.h_aff = b.take<uint32_t>(48 * n);
-  w.f = b.take<uint32_t>(144 * n);
+  w.pk_aff = b.take<uint32_t>(2 * FP_LIMBS * n);
+  w.sig_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
+  w.h_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
+  w.f = b.take<uint32_t>(12 * FP_LIMBS * n);
   w.pk_st = b.take<uint8_t>(n);
   w.sig_st = b.take<uint8_t>(n);
   w.f_st = b.take<uint8_t>(n);
@@ -211,7 +212,7 @@ AggPlan plan_agg(size_t ng, const uint32_t* offsets) {
 
 size_t agg_ws_size(const AggPlan& p, int ncomp) {
   size_t s = 1024;
-  for (auto& lv : p.levels) s += align256(lv.size() * sizeof(agg_chunk)) + align256(lv.size() * ncomp * 48) + align256(lv.size());
+  for (auto& lv : p.levels) s += align256(lv.size() * sizeof(agg_chunk)) + align256(lv.size() * ncomp * FPW) + align256(lv.size());
   return s;
 }
 
@@ -226,7 +227,7 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
   for (size_t l = 0; l < p.levels.size(); ++l) {
     const auto& lv = p.levels[l];
     agg_chunk* d_chunks = b.take<agg_chunk>(lv.size());
-    uint32_t* jac = b.take<uint32_t>(lv.size() * soa_jac<F>::NC * 12);
+    uint32_t* jac = b.take<uint32_t>(lv.size() * soa_jac<F>::NC * FP_LIMBS);
     uint8_t* bad = b.take<uint8_t>(lv.size());
     HIPC(hipMemcpyAsync(d_chunks, lv.data(), lv.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
     if (l == 0) {
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(KBLOCK) k_fp12_pair_product_st(size_t m, const
 int reduce_fp12(size_t m, uint32_t* f, uint8_t* st, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st) {
   while (m > 1) {
     const size_t half = (m + 1) / 2;
-    uint32_t* nf = b.take<uint32_t>(144 * half);
+    uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * half);
     uint8_t* nst = b.take<uint8_t>(half);
     LAUNCH("fp12_product", s, dim3(grid_for(half)), dim3(KBLOCK), k_fp12_pair_product_st, m, (const uint32_t*)f,
            (const uint8_t*)st, nf, nst);
@@ -364,7 +365,7 @@ int vm_partial(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, size_t
   HIPC(hipMemcpyAsync(d_sig, sig, 96, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_dom, dom8, 8, hipMemcpyHostToDevice, s));
   // group sums -> affine + subgroup check
-  uint32_t* agg_aff = b.take<uint32_t>(24 * (G + 1));
+  uint32_t* agg_aff = b.take<uint32_t>(2 * FP_LIMBS * (G + 1));
   uint8_t* agg_st = b.take<uint8_t>(G + 1);
   if (G > 0) {
     const uint32_t* jac;
@@ -377,19 +378,19 @@ int vm_partial(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, size_t
     LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
   }
   // hashes of distinct messages
-  uint32_t* h_aff = b.take<uint32_t>(48 * (G + 1));
+  uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
   uint8_t* h_st = b.take<uint8_t>(G + 1);
   if (G > 0)
     LAUNCH("hash_to_g2", s, dim3(grid_for(G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
            (const uint8_t*)d_dom, 0, h_aff, h_st);
   // signature
-  uint32_t* sig_aff = b.take<uint32_t>(48);
+  uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS);
   uint8_t* sig_st = b.take<uint8_t>(1);
   LAUNCH("decode_g2", s, dim3(1), dim3(KBLOCK), k_decode_g2, (size_t)1, (const uint8_t*)d_sig, sig_aff, sig_st, 1);
   const size_t np = G + (with_sig ? 1 : 0);
   if (np == 0) {
     // empty product: f = 1 (py_ecc's FQ12.one() start value)
-    uint32_t* f = b.take<uint32_t>(144);
+    uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS);
     uint8_t* st = b.take<uint8_t>(1);
     std::vector<uint8_t> one(576, 0);
     one[47] = 1;
@@ -403,7 +404,7 @@ int vm_partial(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, size_t
     *d_st = st;
     return 0;
   }
-  uint32_t* f = b.take<uint32_t>(144 * np);
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * np);
   uint8_t* st = b.take<uint8_t>(np);
   LAUNCH("miller_loop_1", s, dim3(grid_for(np)), dim3(KBLOCK), k_miller_vm, G, with_sig, (const uint32_t*)h_aff,
          (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, (const uint32_t*)sig_aff,
@@ -415,9 +416,9 @@ size_t vm_ws_bound(size_t n, size_t mlen) {
   // generous bound: inputs + per-group buffers + agg levels + Miller tree
   const size_t G = n + 1;
   return 4096 + align256(48 * n) + align256(mlen * n) + 2 * 1024 +
-         align256(24 * 4 * G) + align256(G) + align256(48 * 4 * G) + align256(G) + 1024 +
-         3 * (align256(144 * 4 * G) + align256(G)) + 2 * (align256(G * 12) + align256(G * 36 * 4) + align256(G)) +
-         (size_t)(2 * G / (CHUNK_L1) + 64) * (36 * 4 + 16);
+         align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G) + 1024 +
+         3 * (align256(12 * FPW * G) + align256(G)) + 2 * (align256(G * 12) + align256(G * 3 * FPW) + align256(G)) +
+         (size_t)(2 * G / (CHUNK_L1) + 64) * (3 * FPW + 16);
 }
 
 }  // namespace
@@ -596,11 +597,11 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) {
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  if ((rc = ensure_ws(c, 4 * (align256(576 * k) + align256(144 * 4 * k) + align256(k)) + 8192))) return rc;
+  if ((rc = ensure_ws(c, 4 * (align256(576 * k) + align256(12 * FPW * k) + align256(k)) + 8192))) return rc;
   Bump b(c->ws);
   hipStream_t s = c->stream;
   uint8_t* d_in = b.take<uint8_t>(576 * k);
-  uint32_t* f = b.take<uint32_t>(144 * k);
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * k);
   uint8_t* st = b.take<uint8_t>(k);
   HIPC(hipMemcpyAsync(d_in, parts576, 576 * k, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(st, 0, k, s));
@@ -644,7 +645,7 @@ static size_t agg_ws_bytes(int is_g2, size_t ng, const uint32_t* offsets) {
 size_t bls381_aggregate_pubkeys_batch_workspace_size(size_t n_groups, size_t n_pks) {
   // worst case chunking: every group splits into ceil(size/CHUNK) chunks, plus levels
   const size_t chunks = n_groups + n_pks / CHUNK_L1 + 1;
-  return 8192 + 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * 48) + align256(chunks));
+  return 8192 + 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks));
 }
 
 int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_offsets, size_t n_pks,
@@ -820,7 +821,7 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  const size_t scratch = (size_t)n * H2_BITS * 6 * 12 * 4;
+  const size_t scratch = (size_t)n * H2_BITS * 6 * FPW;
   if ((rc = ensure_ws(c, align256(32 * n) + align256(8 * n) + align256(288 * n) + align256(scratch) + 4096))) return rc;
   Bump b(c->ws);
   uint8_t* d_msgs = b.take<uint8_t>(32 * n);

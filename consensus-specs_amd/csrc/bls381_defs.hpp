@@ -18,8 +18,14 @@
 
 namespace bls381 {
 
-// Fp element: 12 x 32-bit limbs, little-endian, Montgomery form (R = 2^384)
-struct fp_t { uint32_t w[12]; };
+// Fp element: 14 limbs of 28 bits held in u32 words, little-endian, Montgomery
+// form with R = 2^392.  Stored values keep every limb < 2^28 and value < 2q
+// (DESIGN.md "Fp representation"); Fp multiplication accumulates each 28x28-bit
+// partial product in place into a 64-bit column (one v_mad_u64_u32 per product).
+constexpr int FP_LIMBS = 14;
+constexpr int FP_BITS = 28;
+constexpr uint32_t FP_MASK = (1u << 28) - 1;
+struct fp_t { uint32_t w[14]; };
 // Fp2 = Fp[u]/(u^2+1): c0 + c1 u
 struct fp2_t { fp_t c0, c1; };
 // Fp6 = Fp2[v]/(v^3 - (1+u))

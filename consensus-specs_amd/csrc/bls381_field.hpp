@@ -1,8 +1,8 @@
 // BLS12-381 base field Fp and the tower Fp2 / Fp6 / Fp12.
 //
-// Fp: 12 x u32 limbs, Montgomery form R = 2^384.  Multiplication is the
-// "no-carry" CIOS variant (valid because q's top limb 0x1a0111ea < 2^31 - 2):
-// one v_mad_u64_u32 per 32x32 partial product, limbs stay in VGPRs.
+// Fp: 14 limbs x 28 bits, Montgomery form R = 2^392.  Every 28x28-bit partial
+// product accumulates in place into a 64-bit column (one v_mad_u64_u32, no
+// carry chain); carries are resolved once per reduction row.
 // Tower (DESIGN.md "Data layout"):  Fp2 = Fp[u]/(u^2+1),
 // Fp6 = Fp2[v]/(v^3 - (1+u)),  Fp12 = Fp6[w]/(w^2 - v)  (w^6 = 1+u).
 // Algorithms are mirrored 1:1 by oracle/tower_model.py (test infrastructure).
@@ -21,132 +21,176 @@ inline thread_local uint64_t g_fp_mul_count = 0;
 #endif
 
 // ----------------------------------------------------------------- Fp -----
-BLS_INLINE fp_t fp_zero() { fp_t r; for (int i = 0; i < 12; ++i) r.w[i] = 0; return r; }
+// Invariant for every fp_t crossing a function boundary: limbs < 2^28
+// ("normalized") and value < 2q ("weakly reduced").  Canonical (< q) form is
+// produced only where bits matter (codecs, comparisons).
+BLS_INLINE fp_t fp_zero() { fp_t r; for (int i = 0; i < 14; ++i) r.w[i] = 0; return r; }
 BLS_INLINE fp_t fp_one() { return FP_ONE_M; }
 
-BLS_INLINE bool fp_is_zero(const fp_t& a) {
-  uint32_t acc = 0;
+// signed carry propagation: limbs -> [0, 2^28) except the top limb, which
+// keeps the (possibly negative) high part
+BLS_INLINE void fp_carry(int32_t (&t)[14]) {
 #pragma unroll
-  for (int i = 0; i < 12; ++i) acc |= a.w[i];
-  return acc == 0;
-}
-
-BLS_INLINE bool fp_eq(const fp_t& a, const fp_t& b) {
-  uint32_t acc = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) acc |= a.w[i] ^ b.w[i];
-  return acc == 0;
-}
-
-// r = s - q if s >= q else s   (s < 2q)
-BLS_INLINE fp_t fp_reduce_once(const fp_t& s) {
-  fp_t d;
-  uint32_t br = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)s.w[i] - Q_LIMBS[i] - br;
-    d.w[i] = (uint32_t)t;
-    br = (uint32_t)(t >> 63);
+  for (int i = 0; i < 13; ++i) {
+    t[i + 1] += t[i] >> 28;
+    t[i] &= (int32_t)FP_MASK;
   }
+}
+
+// given s (value < 4q, limbs < 2^29): return s mod 2q in normalized form
+BLS_INLINE fp_t fp_fold_2q(const int32_t (&s)[14]) {
+  int32_t a[14], b[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) { a[i] = s[i]; b[i] = s[i] - (int32_t)Q2_LIMBS[i]; }
+  fp_carry(a);
+  fp_carry(b);
+  const bool neg = b[13] < 0;   // s < 2q
   fp_t r;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) r.w[i] = br ? s.w[i] : d.w[i];
+  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(neg ? a[i] : b[i]);
   return r;
 }
 
 BLS_INLINE fp_t fp_add(const fp_t& a, const fp_t& b) {
-  fp_t s;
-  uint32_t c = 0;
+  int32_t s[14];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.w[i] + b.w[i] + c;
-    s.w[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
-  return fp_reduce_once(s);
+  for (int i = 0; i < 14; ++i) s[i] = (int32_t)(a.w[i] + b.w[i]);
+  return fp_fold_2q(s);
 }
 
+// a - b for a, b < 2q: d in (-2q, 2q); add 2q when negative
 BLS_INLINE fp_t fp_sub(const fp_t& a, const fp_t& b) {
-  fp_t d;
-  uint32_t br = 0;
+  int32_t d[14], e[14];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.w[i] - b.w[i] - br;
-    d.w[i] = (uint32_t)t;
-    br = (uint32_t)(t >> 63);
+  for (int i = 0; i < 14; ++i) {
+    d[i] = (int32_t)a.w[i] - (int32_t)b.w[i];
+    e[i] = d[i] + (int32_t)Q2_LIMBS[i];
   }
-  // if borrow: d += q
-  fp_t e;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)d.w[i] + (br ? Q_LIMBS[i] : 0u) + c;
-    e.w[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
-  return e;
-}
-
-BLS_INLINE fp_t fp_neg(const fp_t& a) {
-  fp_t z = fp_zero();
-  return fp_sub(z, a);
-}
-
-BLS_INLINE fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
-
-// a / 2 mod q
-BLS_INLINE fp_t fp_half(const fp_t& a) {
-  const uint32_t odd = a.w[0] & 1u;
-  fp_t s;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.w[i] + (odd ? Q_LIMBS[i] : 0u) + c;
-    s.w[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
+  fp_carry(d);
+  fp_carry(e);
+  const bool neg = d[13] < 0;
   fp_t r;
 #pragma unroll
-  for (int i = 0; i < 11; ++i) r.w[i] = (s.w[i] >> 1) | (s.w[i + 1] << 31);
-  r.w[11] = (s.w[11] >> 1) | (c << 31);
+  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(neg ? e[i] : d[i]);
   return r;
 }
 
-// Montgomery product a * b * R^-1 mod q, inputs < q, output < q.
-BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) {
-  BLS_COUNT_FP_MUL();
-  uint32_t t[12];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) t[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const uint32_t bi = b.w[i];
-    uint64_t s = (uint64_t)a.w[0] * bi + t[0];
-    uint32_t A = (uint32_t)(s >> 32);
-    const uint32_t t0 = (uint32_t)s;
-    const uint32_t m = t0 * Q_INV32;
-    uint64_t s2 = (uint64_t)m * Q_LIMBS[0] + t0;
-    uint32_t C = (uint32_t)(s2 >> 32);
-#pragma unroll
-    for (int j = 1; j < 12; ++j) {
-      s = (uint64_t)a.w[j] * bi + t[j] + A;
-      A = (uint32_t)(s >> 32);
-      s2 = (uint64_t)m * Q_LIMBS[j] + (uint32_t)s + C;
-      C = (uint32_t)(s2 >> 32);
-      t[j - 1] = (uint32_t)s2;
-    }
-    t[11] = C + A;
-  }
+BLS_INLINE fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
+BLS_INLINE fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
+
+// lazy sum for a multiplication operand only: limbs < 2^29, value < 4q
+BLS_INLINE fp_t fp_add_lazy(const fp_t& a, const fp_t& b) {
   fp_t r;
 #pragma unroll
-  for (int i = 0; i < 12; ++i) r.w[i] = t[i];
-  return fp_reduce_once(r);
+  for (int i = 0; i < 14; ++i) r.w[i] = a.w[i] + b.w[i];
+  return r;
 }
 
-BLS_INLINE fp_t fp_sqr(const fp_t& a) { return fp_mul(a, a); }
+// value < 2q -> value < q (canonical)
+BLS_INLINE fp_t fp_reduce_once(const fp_t& s) {
+  int32_t b[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) b[i] = (int32_t)s.w[i] - (int32_t)Q_LIMBS[i];
+  fp_carry(b);
+  const bool neg = b[13] < 0;
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.w[i] = neg ? s.w[i] : (uint32_t)b[i];
+  return r;
+}
 
+// value < 2q: zero mod q  <=>  value == 0 or value == q
+BLS_INLINE bool fp_is_zero(const fp_t& a) {
+  uint32_t z = 0, e = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) { z |= a.w[i]; e |= a.w[i] ^ Q_LIMBS[i]; }
+  return z == 0 || e == 0;
+}
+
+BLS_INLINE bool fp_eq(const fp_t& a, const fp_t& b) { return fp_is_zero(fp_sub(a, b)); }
+
+// a / 2 mod q (value < 2q in, value < 1.5q out)
+BLS_INLINE fp_t fp_half(const fp_t& a) {
+  const uint32_t odd = a.w[0] & 1u;
+  int32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = (int32_t)(a.w[i] + (odd ? Q_LIMBS[i] : 0u));
+  fp_carry(s);
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 13; ++i) r.w[i] = ((uint32_t)s[i] >> 1) | (((uint32_t)s[i + 1] & 1u) << 27);
+  r.w[13] = (uint32_t)s[13] >> 1;
+  return r;
+}
+
+// Montgomery product a * b * 2^-392 mod q.  Inputs: limbs < 2^30 and
+// value(a) * value(b) < 2900 q^2 (e.g. both < 4q lazily summed).  Output:
+// normalized, value < 2q.  Column k accumulates <= 14 products < 2^60 plus
+// <= 14 reduction products < 2^56 and a carry < 2^36: < 2^64.
+BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) {
+  BLS_COUNT_FP_MUL();
+  uint64_t T[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) T[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[i + j] += (uint64_t)a.w[i] * b.w[j];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const uint32_t m = ((uint32_t)T[i] * Q_INV28) & FP_MASK;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[i + j] += (uint64_t)m * Q_LIMBS[j];
+    T[i + 1] += T[i] >> 28;
+  }
+  fp_t r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    const uint64_t v = T[14 + j] + c;
+    r.w[j] = (uint32_t)v & FP_MASK;
+    c = v >> 28;
+  }
+  return r;
+}
+
+// squaring: 105 products instead of 196 (cross products doubled via 2a_i)
+BLS_NOINLINE fp_t fp_sqr(fp_t a) {
+  BLS_COUNT_FP_MUL();
+  uint64_t T[28];
+  uint32_t a2[14];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) T[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) a2[i] = a.w[i] << 1;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    T[2 * i] += (uint64_t)a.w[i] * a.w[i];
+#pragma unroll
+    for (int j = i + 1; j < 14; ++j) T[i + j] += (uint64_t)a2[i] * a.w[j];
+  }
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const uint32_t m = ((uint32_t)T[i] * Q_INV28) & FP_MASK;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[i + j] += (uint64_t)m * Q_LIMBS[j];
+    T[i + 1] += T[i] >> 28;
+  }
+  fp_t r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    const uint64_t v = T[14 + j] + c;
+    r.w[j] = (uint32_t)v & FP_MASK;
+    c = v >> 28;
+  }
+  return r;
+}
+
+// k * a for a small constant k (k * 2q < 2^31): limb scale, then reduce mod 2q
 BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
-  // k in {2,3,4,8,...}: small constant multiples by addition chains
+  // k*a < 2kq; fold by repeated conditional subtraction of 2q is k/2 steps --
+  // instead multiply by k in Montgomery form via an addition chain of fp_add
   fp_t r = a;
   fp_t acc = fp_zero();
   bool first = true;
@@ -158,7 +202,7 @@ BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
   return acc;
 }
 
-// left-to-right square-and-multiply over a 12-limb little-endian exponent
+// left-to-right square-and-multiply over a 12-word little-endian (u32) exponent
 BLS_HD inline fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
   fp_t r = FP_ONE_M;
   for (int i = nbits - 1; i >= 0; --i) {
@@ -177,66 +221,74 @@ BLS_HD inline bool fp_sqrt(fp_t& r, const fp_t& a) {
 }
 
 BLS_INLINE fp_t fp_to_mont(const fp_t& plain) { return fp_mul(plain, FP_R2); }
+// Montgomery -> canonical plain value (< q)
 BLS_INLINE fp_t fp_from_mont(const fp_t& m) {
   fp_t one = fp_zero();
   one.w[0] = 1;
-  return fp_mul(m, one);
+  return fp_reduce_once(fp_mul(m, one));
 }
 
-// plain (non-Montgomery) comparisons and byte codecs
+// ---- plain (canonical, normalized) values: comparisons and byte codecs
+// a < q
 BLS_INLINE bool fp_plain_lt_q(const fp_t& a) {
-  uint32_t br = 0;
+  int32_t b[14];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)a.w[i] - Q_LIMBS[i] - br;
-    br = (uint32_t)(t >> 63);
-  }
-  return br != 0;
+  for (int i = 0; i < 14; ++i) b[i] = (int32_t)a.w[i] - (int32_t)Q_LIMBS[i];
+  fp_carry(b);
+  return b[13] < 0;
 }
 
-// a > b for plain values
+// a > b
 BLS_INLINE bool fp_plain_gt(const fp_t& a, const fp_t& b) {
-  uint32_t br = 0;
+  int32_t d[14];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)b.w[i] - a.w[i] - br;
-    br = (uint32_t)(t >> 63);
-  }
-  return br != 0;  // b - a borrows  <=>  b < a
+  for (int i = 0; i < 14; ++i) d[i] = (int32_t)b.w[i] - (int32_t)a.w[i];
+  fp_carry(d);
+  return d[13] < 0;
 }
 
 // (2*y) // q == 1  <=>  2y >= q, for plain y < q (spec a_flag, bls_signature.md:52)
 BLS_INLINE bool fp_plain_is_upper_half(const fp_t& y) {
-  uint32_t c = 0;
-  fp_t s;
+  int32_t b[14];
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    uint64_t t = (uint64_t)y.w[i] + y.w[i] + c;
-    s.w[i] = (uint32_t)t;
-    c = (uint32_t)(t >> 32);
-  }
-  return !fp_plain_lt_q(s);
+  for (int i = 0; i < 14; ++i) b[i] = (int32_t)(2 * y.w[i]) - (int32_t)Q_LIMBS[i];
+  fp_carry(b);
+  return b[13] >= 0;
 }
 
-// 48 big-endian bytes -> plain limbs (no reduction)
+// 48 big-endian bytes -> plain limbs (no reduction; value < 2^384)
 BLS_INLINE fp_t fp_plain_from_be48(const uint8_t* p) {
-  fp_t r;
+  uint32_t w[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
     const uint8_t* b = p + 44 - 4 * i;
-    r.w[i] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+    w[i] = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  }
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int bit = 28 * k, wi = bit >> 5, sh = bit & 31;
+    uint64_t v = (uint64_t)w[wi] >> sh;
+    if (wi + 1 < 12) v |= (uint64_t)w[wi + 1] << (32 - sh);
+    r.w[k] = (uint32_t)v & FP_MASK;
   }
   return r;
 }
 
+// plain canonical value -> 48 big-endian bytes
 BLS_INLINE void fp_plain_to_be48(uint8_t* p, const fp_t& a) {
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
+    const int bit = 32 * i, k = bit / 28, sh = bit % 28;
+    uint64_t v = (uint64_t)a.w[k] >> sh;
+    if (k + 1 < 14) v |= (uint64_t)a.w[k + 1] << (28 - sh);
+    if (k + 2 < 14 && 56 - sh < 32) v |= (uint64_t)a.w[k + 2] << (56 - sh);
+    const uint32_t w = (uint32_t)v;
     uint8_t* b = p + 44 - 4 * i;
-    b[0] = (uint8_t)(a.w[i] >> 24);
-    b[1] = (uint8_t)(a.w[i] >> 16);
-    b[2] = (uint8_t)(a.w[i] >> 8);
-    b[3] = (uint8_t)a.w[i];
+    b[0] = (uint8_t)(w >> 24);
+    b[1] = (uint8_t)(w >> 16);
+    b[2] = (uint8_t)(w >> 8);
+    b[3] = (uint8_t)w;
   }
 }
 
@@ -256,7 +308,7 @@ BLS_INLINE fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { fp2_t r; r.c0 = fp_
 BLS_INLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   const fp_t t0 = fp_mul(a.c0, b.c0);
   const fp_t t1 = fp_mul(a.c1, b.c1);
-  const fp_t t2 = fp_mul(fp_add(a.c0, a.c1), fp_add(b.c0, b.c1));
+  const fp_t t2 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_add_lazy(b.c0, b.c1));
   fp2_t r;
   r.c0 = fp_sub(t0, t1);
   r.c1 = fp_sub(fp_sub(t2, t0), t1);
@@ -265,7 +317,7 @@ BLS_INLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
 
 BLS_INLINE fp2_t fp2_sqr(const fp2_t& a) {
   fp2_t r;
-  r.c0 = fp_mul(fp_add(a.c0, a.c1), fp_sub(a.c0, a.c1));
+  r.c0 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_sub(a.c0, a.c1));
   const fp_t t = fp_mul(a.c0, a.c1);
   r.c1 = fp_add(t, t);
   return r;

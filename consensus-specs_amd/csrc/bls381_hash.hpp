@@ -67,9 +67,13 @@ BLS_HD inline void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
 
 // 8 big-endian digest words -> plain Fp limbs (256-bit value < q)
 BLS_INLINE fp_t fp_plain_from_digest(const uint32_t d[8]) {
-  fp_t r = fp_zero();
-  for (int i = 0; i < 8; ++i) r.w[i] = d[7 - i];
-  return r;
+  uint8_t b[48];
+  for (int i = 0; i < 16; ++i) b[i] = 0;
+  for (int i = 0; i < 8; ++i) {
+    b[16 + 4 * i] = (uint8_t)(d[i] >> 24); b[17 + 4 * i] = (uint8_t)(d[i] >> 16);
+    b[18 + 4 * i] = (uint8_t)(d[i] >> 8); b[19 + 4 * i] = (uint8_t)d[i];
+  }
+  return fp_plain_from_be48(b);
 }
 
 // spec root selection (bls_signature.md:91,107): keep the root whose imaginary

@@ -1,6 +1,6 @@
 // gfx950 kernels of the BLS12-381 engine.  One work item per lane; every
 // intermediate lives in HBM in structure-of-arrays, limb-major layout
-// (limb k of component c of item i at base[(c*12 + k) * n + i]) so that each
+// (limb k of component c of item i at base[(c*14 + k) * n + i]) so that each
 // limb load/store of a wavefront is one contiguous 256-byte access
 // (DESIGN.md "Data layout in HBM").
 #pragma once
@@ -17,12 +17,12 @@ constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 __device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
   fp_t r;
 #pragma unroll
-  for (int k = 0; k < 12; ++k) r.w[k] = p[(size_t)(c * 12 + k) * n + i];
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = p[(size_t)(c * FP_LIMBS + k) * n + i];
   return r;
 }
 __device__ __forceinline__ void soa_st(uint32_t* __restrict__ p, size_t n, size_t i, int c, const fp_t& a) {
 #pragma unroll
-  for (int k = 0; k < 12; ++k) p[(size_t)(c * 12 + k) * n + i] = a.w[k];
+  for (int k = 0; k < FP_LIMBS; ++k) p[(size_t)(c * FP_LIMBS + k) * n + i] = a.w[k];
 }
 __device__ __forceinline__ fp2_t soa_ld2(const uint32_t* p, size_t n, size_t i, int c) {
   fp2_t r; r.c0 = soa_ld(p, n, i, c); r.c1 = soa_ld(p, n, i, c + 1); return r;

@@ -41,13 +41,29 @@ def test_fp_ops(L):
         L.hc_fp_add(b48(a), b48(b), buf); assert i48(buf.raw) == (a + b) % q
         L.hc_fp_sub(b48(a), b48(b), buf); assert i48(buf.raw) == (a - b) % q
         L.hc_fp_half(b48(a), buf); assert i48(buf.raw) * 2 % q == a
-    # raw Montgomery product stays < q for all inputs < q
-    R = 1 << 384
+    # raw Montgomery product (R = 2^392): weakly reduced output < 2q, congruent
+    R = 1 << 392
     Rinv = pow(R, -1, q)
-    for _ in range(100):
-        a, b = rng.randrange(q), rng.randrange(q)
+    for i in range(200):
+        a, b = (rng.randrange(q), rng.randrange(q)) if i > 1 else (q - 1, q - 1)
         L.hc_fp_mont_mul_raw(b48(a), b48(b), buf)
-        assert i48(buf.raw) == a * b * Rinv % q
+        v = i48(buf.raw)
+        assert v < 2 * q and v % q == a * b * Rinv % q
+
+
+def test_fp_mul_extreme_operands(L):
+    """fp_mul accepts any operands with limbs < 2^28 and value < 2^384 (< 9.6q):
+    output must stay < 2q and congruent (column sums stay < 2^64)."""
+    rng = random.Random(15)
+    buf = ctypes.create_string_buffer(48)
+    Rinv = pow(1 << 392, -1, q)
+    top = (1 << 384) - 1
+    cases = [(top, top), (top, 0), (2 * q - 1, 2 * q - 1), (q, q), (top, 1)]
+    cases += [(rng.randrange(1 << 384), rng.randrange(1 << 384)) for _ in range(300)]
+    for a, b in cases:
+        L.hc_fp_mont_mul_raw(b48(a), b48(b), buf)
+        v = i48(buf.raw)
+        assert v < 2 * q and v % q == a * b * Rinv % q
 
 
 def test_fp_inv_sqrt(L):

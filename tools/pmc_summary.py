@@ -1,0 +1,63 @@
+"""Aggregate rocprofv3 --pmc CSV passes per kernel (last dispatch of each kernel).
+
+Usage: python tools/pmc_summary.py gpurun_out/pmc_TAG [out.md]
+"""
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(k_[A-Za-z0-9_]+)", name)
+    return m.group(1) if m else name[:50]
+
+
+def main():
+    d = sys.argv[1]
+    data = defaultdict(dict)     # kernel -> counter -> value (last dispatch)
+    last_disp = defaultdict(dict)
+    for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row["Kernel_Name"])
+                c = row["Counter_Name"]
+                disp = int(row["Dispatch_Id"])
+                v = float(row["Counter_Value"])
+                key = (k, c)
+                prev = last_disp[k].get(c)
+                if prev is None or disp > prev[0]:
+                    last_disp[k][c] = (disp, v)
+                elif disp == prev[0]:
+                    last_disp[k][c] = (disp, prev[1] + v)   # sum over dimensions
+    for k, cs in last_disp.items():
+        for c, (disp, v) in cs.items():
+            data[k][c] = v
+    cols = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_SALU",
+            "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_FLAT", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+            "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+            "GRBM_GUI_ACTIVE", "FETCH_SIZE", "WRITE_SIZE"]
+    kernels = [k for k in data if k.startswith("k_")]
+    lines = ["| counter | " + " | ".join(kernels) + " |", "|---|" + "---|" * len(kernels)]
+    for c in cols:
+        lines.append("| %s | " % c + " | ".join("%.4g" % data[k].get(c, float("nan")) for k in kernels) + " |")
+    # derived
+    lines.append("| VALU insts / wave | " + " | ".join(
+        "%.4g" % (data[k].get("SQ_INSTS_VALU", 0) / max(data[k].get("SQ_WAVES", 1), 1)) for k in kernels) + " |")
+    lines.append("| VMEM (rd+wr) / VALU | " + " | ".join(
+        "%.3f" % ((data[k].get("SQ_INSTS_VMEM_RD", 0) + data[k].get("SQ_INSTS_VMEM_WR", 0)) /
+                  max(data[k].get("SQ_INSTS_VALU", 1), 1)) for k in kernels) + " |")
+    lines.append("| WAIT_ANY / WAVE_CYCLES | " + " | ".join(
+        "%.3f" % (data[k].get("SQ_WAIT_ANY", 0) / max(data[k].get("SQ_WAVE_CYCLES", 1), 1)) for k in kernels) + " |")
+    lines.append("| HBM bytes (2*FETCH_KB*1024 + WRITE_KB*1024) | " + " | ".join(
+        "%.4g" % (2 * data[k].get("FETCH_SIZE", 0) * 1024 + data[k].get("WRITE_SIZE", 0) * 1024) for k in kernels) + " |")
+    out = "\n".join(lines)
+    print(out)
+    if len(sys.argv) > 2:
+        open(sys.argv[2], "w").write(out + "\n")
+
+
+if __name__ == "__main__":
+    main()
