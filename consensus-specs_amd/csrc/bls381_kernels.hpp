@@ -12,6 +12,11 @@ namespace bls381 {
 enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2 };
 
 constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
+// minimum waves per SIMD requested from the register allocator for the heavy
+// per-item kernels (1 = up to 512 VGPR+AGPR per lane, 2 = up to 256)
+#ifndef BLS_WAVES_PER_EU
+#define BLS_WAVES_PER_EU 1
+#endif
 
 // ------------------------------------------------------------ SoA access --
 __device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
@@ -78,7 +83,7 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
 
 // --------------------------------------------------------- decode kernels --
 // pubkeys -> affine G1 (SoA 2 Fp) + status; optional subgroup check
-__global__ void __launch_bounds__(KBLOCK) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      int check_subgroup) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -93,7 +98,7 @@ __global__ void __launch_bounds__(KBLOCK) k_decode_g1(size_t n, const uint8_t* _
 }
 
 // signatures -> affine G2 (SoA 4 Fp) + status; optional subgroup check
-__global__ void __launch_bounds__(KBLOCK) k_decode_g2(size_t n, const uint8_t* __restrict__ sigs,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n, const uint8_t* __restrict__ sigs,
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      int check_subgroup) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,7 +113,7 @@ __global__ void __launch_bounds__(KBLOCK) k_decode_g2(size_t n, const uint8_t* _
 }
 
 // (msg, dom8) -> hash_to_G2 affine (SoA 4 Fp).  dom_stride 0 = one shared domain.
-__global__ void __launch_bounds__(KBLOCK) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                    const uint8_t* __restrict__ doms, int dom_stride,
                                                    uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(KBLOCK) k_hash_g2(size_t n, const uint8_t* __r
 // --------------------------------------------------------- verify kernels --
 // One bls_verify per lane: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
 // infinity short-circuit of py_ecc's pairing (a pair with an infinite point is 1).
-__global__ void __launch_bounds__(KBLOCK) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
                                                          const uint8_t* __restrict__ sig_st,
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const uint8_t* __restrict__ pk_st,
@@ -159,7 +164,7 @@ __global__ void __launch_bounds__(KBLOCK) k_miller_verify(size_t n, const uint32
   st_out[i] = ST_OK;
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
