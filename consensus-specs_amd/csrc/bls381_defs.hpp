@@ -5,11 +5,18 @@
 
 #if defined(__HIP__)
 #include <hip/hip_runtime.h>
+// keep the scheduler from interleaving independent phases (bounds live ranges)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define BLS_PHASE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define BLS_PHASE() ((void)0)
+#endif
 #define BLS_HD __host__ __device__
 #define BLS_INLINE __host__ __device__ __forceinline__
 #define BLS_NOINLINE __host__ __device__ __attribute__((noinline))
 #define BLS_CONST __device__ __constant__ static constexpr
 #else
+#define BLS_PHASE() ((void)0)
 #define BLS_HD
 #define BLS_INLINE inline __attribute__((always_inline))
 #define BLS_NOINLINE __attribute__((noinline))

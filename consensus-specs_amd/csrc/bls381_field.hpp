@@ -305,22 +305,81 @@ BLS_INLINE fp2_t fp2_half(const fp2_t& a) { fp2_t r; r.c0 = fp_half(a.c0); r.c1 
 BLS_INLINE fp2_t fp2_conj(const fp2_t& a) { fp2_t r; r.c0 = a.c0; r.c1 = fp_neg(a.c1); return r; }
 BLS_INLINE fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { fp2_t r; r.c0 = fp_mul(a.c0, b); r.c1 = fp_mul(a.c1, b); return r; }
 
+// ---- double-width (28-column) helpers for lazy reduction
+// T[k] += sum_{i+j=k} a_i b_j   (operand limbs < 2^30)
+BLS_INLINE void wide_mac(uint64_t (&T)[28], const fp_t& a, const fp_t& b) {
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[i + j] += (uint64_t)a.w[i] * b.w[j];
+}
+
+// T[k] += columns of a^2 (operand limbs < 2^29)
+BLS_INLINE void wide_sqr(uint64_t (&T)[28], const fp_t& a) {
+  uint32_t a2[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) a2[i] = a.w[i] << 1;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    T[2 * i] += (uint64_t)a.w[i] * a.w[i];
+#pragma unroll
+    for (int j = i + 1; j < 14; ++j) T[i + j] += (uint64_t)a2[i] * a.w[j];
+  }
+}
+
+// Montgomery reduction of a double-width value: columns < 2^63.2 and value
+// < 2^773 (= q R) -> normalized, value < 2q.
+BLS_INLINE fp_t fp_redc_wide(uint64_t (&T)[28]) {
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const uint32_t m = ((uint32_t)T[i] * Q_INV28) & FP_MASK;
+#pragma unroll
+    for (int j = 0; j < 14; ++j) T[i + j] += (uint64_t)m * Q_LIMBS[j];
+    T[i + 1] += T[i] >> 28;
+  }
+  fp_t r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int j = 0; j < 14; ++j) {
+    const uint64_t v = T[14 + j] + c;
+    r.w[j] = (uint32_t)v & FP_MASK;
+    c = v >> 28;
+  }
+  return r;
+}
+
+// Fp2 product with one REDC per output coefficient (Karatsuba, lazy reduction):
+//   c0 = REDC(a0 b0 + W - a1 b1),  c1 = REDC((a0+a1)(b0+b1) - a0 b0 - a1 b1)
+// W = WIDE_QMULT, a multiple of q whose columns dominate any product column.
+// Inputs may be lazy sums: limbs < 2^29, values < 4q.  Output normalized, < 2q.
+// Fp2 multiplication: three Montgomery products (Karatsuba).  Kept inline so the
+// only call boundary is fp_mul (two 14-word operands in argument registers);
+// measured on MI355X, noinline Fp2-level functions (56-word arguments through
+// the stack plus callee-saved spills) were 15-25 % slower end to end.
+// Operands may be lazy sums (limbs < 2^29, values < 4q): the products see
+// limbs < 2^30 and values < 8q.
 BLS_INLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   const fp_t t0 = fp_mul(a.c0, b.c0);
   const fp_t t1 = fp_mul(a.c1, b.c1);
   const fp_t t2 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_add_lazy(b.c0, b.c1));
   fp2_t r;
   r.c0 = fp_sub(t0, t1);
-  r.c1 = fp_sub(fp_sub(t2, t0), t1);
+  r.c1 = fp_sub(t2, fp_add(t0, t1));
   return r;
 }
 
+// Fp2 squaring: c0 = (a0 + a1)(a0 - a1), c1 = 2 a0 a1 (operands weakly reduced, < 2q)
 BLS_INLINE fp2_t fp2_sqr(const fp2_t& a) {
   fp2_t r;
   r.c0 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_sub(a.c0, a.c1));
   const fp_t t = fp_mul(a.c0, a.c1);
   r.c1 = fp_add(t, t);
   return r;
+}
+
+// lazy Fp2 sum for a multiplication operand only (limbs < 2^29, values < 4q)
+BLS_INLINE fp2_t fp2_add_lazy(const fp2_t& a, const fp2_t& b) {
+  fp2_t r; r.c0 = fp_add_lazy(a.c0, b.c0); r.c1 = fp_add_lazy(a.c1, b.c1); return r;
 }
 
 // multiply by xi = 1 + u
@@ -379,9 +438,9 @@ BLS_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
   const fp2_t t1 = fp2_mul(a.c1, b.c1);
   const fp2_t t2 = fp2_mul(a.c2, b.c2);
   fp6_t r;
-  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add(a.c1, a.c2), fp2_add(b.c1, b.c2)), fp2_add(t1, t2))));
-  r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
-  r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add(a.c0, a.c2), fp2_add(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b.c1, b.c2)), fp2_add(t1, t2))));
+  r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
+  r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), fp2_add(t0, t2)), t1);
   return r;
 }
 
@@ -473,7 +532,7 @@ BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2
     const fp2_t t0 = fp2_mul(a.c0, c0);
     const fp2_t t1 = fp2_mul(a.c1, c1);
     aA.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, c1)));
-    aA.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(a.c0, a.c1), fp2_add(c0, c1)), t0), t1);
+    aA.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(c0, c1)), t0), t1);
     aA.c2 = fp2_add(t1, fp2_mul(a.c2, c0));
   }
   // bB, B = c2 v
@@ -489,7 +548,7 @@ BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2
     const fp2_t t0 = fp2_mul(s.c0, c0);
     const fp2_t t1 = fp2_mul(s.c1, d1);
     m.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(s.c2, d1)));
-    m.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add(s.c0, s.c1), fp2_add(c0, d1)), t0), t1);
+    m.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(s.c0, s.c1), fp2_add_lazy(c0, d1)), t0), t1);
     m.c2 = fp2_add(t1, fp2_mul(s.c2, c0));
   }
   fp12_t r;

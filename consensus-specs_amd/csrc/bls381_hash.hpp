@@ -110,19 +110,46 @@ BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, ui
   }
 }
 
-// [h2] P with the spec's G2_cofactor (bls_signature.md:71), signed-binary (NAF) digits
+// psi on Jacobian coordinates: (cx conj(X), cy conj(Y), conj(Z))
+BLS_INLINE jac_t<fp2_t> g2_psi_jac(const jac_t<fp2_t>& p) {
+  jac_t<fp2_t> r;
+  r.x = fp2_mul(PSI_CX_M, fp2_conj(p.x));
+  r.y = fp2_mul(PSI_CY_M, fp2_conj(p.y));
+  r.z = fp2_conj(p.z);
+  return r;
+}
+
+// [h2] P for the spec's full G2_cofactor h2 (bls_signature.md:71), exactly.
+// With c = 3(x^2 - 1), the Budroni-Pintore combination
+//   BP(P) = [x^2 - x - 1]P + [x - 1]psi(P) + 2 psi^2(P)  equals  [c h2]P
+// for every P in E'(Fp2), and BP(P) lies in G2 where psi acts as [x].  Hence
+// [h2]P = [c^-1 mod r] BP(P), and c^-1 mod r = sum_i e_i |x|^i with
+// e0 = (|x|+1)/3, e1 = 2e0 - 1, e2 = 2e0 - 2, e3 = e0 - 1, which collapses to
+//   [h2]P = [e0] S - T,  S = Q0 + 2Q1 + 2Q2 + Q3,  T = Q1 + 2Q2 + Q3,
+//   Q_i = (-psi)^i BP(P).
+// ~190 doublings + ~45 additions instead of the 508-doubling ladder; the
+// identity is checked in oracle/tower_model.py and tests/test_tower_model.py.
 BLS_HD inline jac_t<fp2_t> g2_mul_cofactor(const aff_t<fp2_t>& p) {
   aff_t<fp2_t> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
-  jac_t<fp2_t> r = jac_from_aff(p);   // leading NAF digit is +1
-  for (int i = 1; i < H2_NAF_LEN; ++i) {
-    r = jac_dbl(r);
-    const int dg = H2_NAF[i];
-    if (dg > 0) r = jac_add_aff(r, p);
-    else if (dg < 0) r = jac_add_aff(r, np);
+  const jac_t<fp2_t> t1 = jac_mul_u64(p, BLS_X_ABS);                  // [|x|]P = -[x]P
+  jac_t<fp2_t> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
+  Q0 = jac_add(Q0, g2_psi_jac(jac_add_aff(jac_neg(t1), np)));          // + psi([x - 1]P)
+  Q0 = jac_add(Q0, g2_psi_jac(g2_psi_jac(jac_dbl(jac_from_aff(p)))));  // + psi^2(2P)
+  const jac_t<fp2_t> Q1 = jac_neg(g2_psi_jac(Q0));
+  const jac_t<fp2_t> Q2 = jac_neg(g2_psi_jac(Q1));
+  const jac_t<fp2_t> T = jac_add(jac_add(jac_dbl(Q2), Q1), jac_neg(g2_psi_jac(Q2)));   // Q1 + 2Q2 + Q3
+  const jac_t<fp2_t> S = jac_add(jac_add(T, Q1), Q0);
+  const jac_t<fp2_t> nS = jac_neg(S);
+  jac_t<fp2_t> R = S;   // leading NAF digit of e0 is +1
+  for (int i = 1; i < E0_NAF_LEN; ++i) {
+    R = jac_dbl(R);
+    const int dg = E0_NAF[i];
+    if (dg > 0) R = jac_add(R, S);
+    else if (dg < 0) R = jac_add(R, nS);
   }
-  return r;
+  return jac_add(R, jac_neg(T));
 }
 
 // full hash_to_G2 for a 32-byte message; returns false only if the result is infinity

@@ -63,6 +63,14 @@ int hc_fp2_sqrt_select(const uint8_t* a, uint8_t* o) {
   return 1;
 }
 
+// lazy-operand stress: raw (Montgomery-domain) limbs in, operands are the lazy
+// sums X+Y and Z+U (each summand < 2^384 as given); returns raw weakly-reduced limbs
+static fp2_t ldraw2(const uint8_t* p) { fp2_t r; r.c0 = fp_plain_from_be48(p); r.c1 = fp_plain_from_be48(p + 48); return r; }
+static void straw2(uint8_t* p, const fp2_t& a) { fp_plain_to_be48(p, a.c0); fp_plain_to_be48(p + 48, a.c1); }
+void hc_fp2_mul_lazy_raw(const uint8_t* x, const uint8_t* y, const uint8_t* z, const uint8_t* u, uint8_t* o) {
+  straw2(o, fp2_mul(fp2_add_lazy(ldraw2(x), ldraw2(y)), fp2_add_lazy(ldraw2(z), ldraw2(u))));
+}
+
 void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st12(o, fp12_mul(ld12(a), ld12(b))); }
 void hc_fp12_sqr(const uint8_t* a, uint8_t* o) { st12(o, fp12_sqr(ld12(a))); }
 void hc_fp12_inv(const uint8_t* a, uint8_t* o) { st12(o, fp12_inv(ld12(a))); }

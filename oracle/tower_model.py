@@ -435,9 +435,26 @@ def map_candidate(message_hash, dom8: bytes):
         x = add2(x, ONE2)
 
 
+def clear_cofactor_h2(P):
+    """[h2]P exactly, via [c^-1 mod r] BP(P) with c = 3(x^2-1) (device g2_mul_cofactor)."""
+    X = X_ABS
+    e0 = (X + 1) // 3
+    F = Fq2
+    neg = lambda p: jac_neg(F, p)
+    add = lambda a, b: jac_add(F, a, b)
+    t1 = jac_mul(F, P, X)
+    Q0 = add(add(add(jac_mul(F, t1, X), t1), neg(P)), psi_jac(add(neg(t1), neg(P))))
+    Q0 = add(Q0, psi_jac(psi_jac(jac_dbl(F, P))))
+    Q1 = neg(psi_jac(Q0))
+    Q2 = neg(psi_jac(Q1))
+    T = add(add(jac_dbl(F, Q2), Q1), neg(psi_jac(Q2)))
+    S = add(add(T, Q1), Q0)
+    return add(jac_mul(F, S, e0), neg(T))
+
+
 def hash_to_g2_affine(message_hash, dom8):
     x, y = map_candidate(message_hash, dom8)
-    return jac_to_affine(Fq2, jac_mul_wnaf(Fq2, (x, y, ONE2), O.G2_cofactor))
+    return jac_to_affine(Fq2, clear_cofactor_h2((x, y, ONE2)))
 
 
 # ----------------------------- Miller loop ---------------------------------

@@ -20,7 +20,7 @@ q = O.q
 @pytest.fixture(scope="module")
 def L():
     import build_native
-    return ctypes.CDLL(build_native.build_hostcheck())
+    return ctypes.CDLL(os.environ.get("BLS381_HOSTCHECK_LIB") or build_native.build_hostcheck())
 
 
 def b48(x): return x.to_bytes(48, "big")
@@ -96,6 +96,26 @@ def test_fp2(L):
         assert (e is None) == (s == 0)
         if e is not None:
             assert i96(buf.raw) == e
+
+
+def test_fp2_lazy_operands_at_bounds(L):
+    """Fp2 mul with lazy operands: limbs < 2^29, values < 4q (sums of two
+    weakly reduced < 2q values).  Output must be < 2q and congruent."""
+    rng = random.Random(17)
+    Rinv = pow(1 << 392, -1, q)
+    out = ctypes.create_string_buffer(96)
+    edge = [2 * q - 1, 2 * q - 2, q, q - 1, 0, (1 << 380)]
+    pick = lambda i: edge[i % len(edge)] if i < 24 else rng.randrange(2 * q)
+    for i in range(400):
+        X = (pick(i), pick(i + 1)); Y = (pick(i + 2), pick(i + 3))
+        Z = (pick(i + 4), pick(i + 5)); U = (pick(i + 6), pick(i + 7))
+        L.hc_fp2_mul_lazy_raw(b96(X), b96(Y), b96(Z), b96(U), out)
+        r0, r1 = i96(out.raw)
+        a = ((X[0] + Y[0]) % q, (X[1] + Y[1]) % q)
+        b = ((Z[0] + U[0]) % q, (Z[1] + U[1]) % q)
+        e = M.mul2(a, b)
+        assert r0 < 2 * q and r1 < 2 * q
+        assert (r0 % q, r1 % q) == (e[0] * Rinv % q, e[1] * Rinv % q)
 
 
 def test_fp12(L):

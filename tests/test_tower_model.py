@@ -42,6 +42,20 @@ def test_pairing_bilinear_and_relation_to_oracle():
     assert M.to_pyecc12(e) == O.f12_pow(O.pairing(O.G2, O.G1), (-3) % O.r)
 
 
+def test_cofactor_clearing_identity():
+    """[h2]P == [e0]S - T (device hash_to_G2 cofactor) on points outside G2; and the
+    Budroni-Pintore combination equals [3(x^2-1) h2]P."""
+    F = M.Fq2
+    for s in range(3):
+        x, y = M.map_candidate(bytes([s]) * 32, b"\x07" * 8)
+        P = (x, y, M.ONE2)
+        want = M.jac_to_affine(F, M.jac_mul(F, P, O.G2_cofactor))
+        assert M.jac_to_affine(F, M.clear_cofactor_h2(P)) == want
+    k = pow(3 * (O.BLS_X ** 2 - 1), -1, O.r)
+    e0 = (M.X_ABS + 1) // 3
+    assert k == e0 + (2 * e0 - 1) * M.X_ABS + (2 * e0 - 2) * M.X_ABS ** 2 + (e0 - 1) * M.X_ABS ** 3
+
+
 def test_hash_sqrt_subgroup_models():
     rng = random.Random(4)
     for i in range(60):
