@@ -47,6 +47,8 @@ _SIGS = {
     "bls381_aggregate_pubkeys_batch_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t, ctypes.c_size_t]),
     "bls381_aggregate_pubkeys_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, _u8p,
                                                              _u8p, _u8p, _u8p]),
+    "bls381_verify_multiple_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, ctypes.c_size_t, _u8p,
+                                                    _u8p, _u8p]),
     "bls381_miller_partial": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int,
                                              _u8p, _u8p]),
     "bls381_final_verify": (ctypes.c_int, [ctypes.c_size_t, _u8p]),
@@ -201,6 +203,16 @@ def aggregate_pubkeys_batch(offsets: np.ndarray, pks: bytes):
     check(lib().bls381_aggregate_pubkeys_batch(ng, offsets.ctypes.data_as(ctypes.c_void_p), _buf(pks), out,
                                                status.ctypes.data_as(ctypes.c_void_p)))
     return [out.raw[48 * g:48 * g + 48] for g in range(ng)], status[:ng]
+
+
+def verify_multiple_batch(call_off, pks: bytes, msgs: bytes, msg_len: int, sigs: bytes, dom8s: bytes) -> np.ndarray:
+    """Batch of bls_verify_multiple calls; call c owns items [call_off[c], call_off[c+1])."""
+    call_off = np.ascontiguousarray(call_off, dtype=np.uint32)
+    nc = len(call_off) - 1
+    out = np.zeros(max(nc, 1), dtype=np.uint8)
+    check(lib().bls381_verify_multiple_batch(nc, call_off.ctypes.data_as(ctypes.c_void_p), _buf(pks), _buf(msgs),
+                                             msg_len, _buf(sigs), _buf(dom8s), out.ctypes.data_as(ctypes.c_void_p)))
+    return out[:nc].astype(bool)
 
 
 def miller_partial(pks: bytes, msgs: bytes, msg_len: int, sig: bytes, include_sig: bool, dom8: bytes):

@@ -8,7 +8,10 @@
 
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <memory>
+#include <stdexcept>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -24,12 +27,22 @@ namespace {
 thread_local std::string t_err;
 thread_local int t_device = -1;
 
+// Host memory that an async copy still reads: released once an event
+// recorded after the copy has completed (device-pointer entry points return
+// without synchronising, so a plan on the C++ stack would die too early).
+struct Keep {
+  hipEvent_t ev;
+  std::shared_ptr<void> data;
+};
+
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   void* ws = nullptr;
   size_t ws_cap = 0;
   std::mutex mu;
+  std::mutex keep_mu;
+  std::deque<Keep> keep;
 };
 
 std::mutex g_mu;
@@ -88,6 +101,25 @@ Ctx* get_ctx(int* rc) {
   return g_ctx[dev];
 }
 
+// Keeps `data` alive until the work queued on `s` so far has completed.
+int keep_until_done(Ctx* c, hipStream_t s, std::shared_ptr<void> data) {
+  std::lock_guard<std::mutex> lk(c->keep_mu);
+  while (!c->keep.empty() && hipEventQuery(c->keep.front().ev) == hipSuccess) {
+    (void)hipEventDestroy(c->keep.front().ev);
+    c->keep.pop_front();
+  }
+  hipEvent_t ev;
+  HIPC(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  hipError_t e = hipEventRecord(ev, s);
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(s);
+    (void)hipEventDestroy(ev);
+    return fail("hipEventRecord", e);
+  }
+  c->keep.push_back({ev, std::move(data)});
+  return 0;
+}
+
 int ensure_ws(Ctx* c, size_t bytes) {
   if (c->ws_cap >= bytes) return 0;
   if (c->ws) { HIPC(hipStreamSynchronize(c->stream)); HIPC(hipFree(c->ws)); c->ws = nullptr; c->ws_cap = 0; }
@@ -97,17 +129,21 @@ int ensure_ws(Ctx* c, size_t bytes) {
   return 0;
 }
 
-// bump allocator over a workspace, 256-byte aligned slices
+// Bump allocator over a workspace (256-byte aligned slices).  Exceeding the
+// capacity throws before anything is launched on the overflowing buffer; ABI
+// entry points map it to an error.
 struct Bump {
   uint8_t* base;
-  size_t off = 0;
-  explicit Bump(void* b) : base((uint8_t*)b) {}
+  size_t off = 0, cap;
+  explicit Bump(void* b, size_t c = SIZE_MAX) : base((uint8_t*)b), cap(c) {}
   template <class T> T* take(size_t count) {
     off = (off + 255) & ~(size_t)255;
+    if (count * sizeof(T) > cap || off > cap - count * sizeof(T)) throw std::length_error("workspace bound exceeded");
     T* p = (T*)(base + off);
     off += count * sizeof(T);
     return p;
   }
+  size_t left() const { return off < cap ? cap - off : 0; }
 };
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 constexpr size_t FPW = 4 * FP_LIMBS;   // bytes per Fp element in SoA buffers
@@ -219,8 +255,8 @@ size_t agg_ws_size(const AggPlan& p, int ncomp) {
 // runs the plan; returns device pointers to the final per-group Jacobian sums / bad flags
 template <class F>
 int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStream_t s,
-            const uint32_t** out_jac, const uint8_t** out_bad, size_t* used) {
-  Bump b(ws);
+            const uint32_t** out_jac, const uint8_t** out_bad, size_t* used, size_t cap = SIZE_MAX) {
+  Bump b(ws, cap);
   const uint32_t* prev_jac = nullptr;
   const uint8_t* prev_bad = nullptr;
   size_t prev_n = 0;
@@ -249,176 +285,210 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
 }
 
 // ------------------------------------------------- verify_multiple pieces --
-// Groups pks by distinct message (first-appearance order), as py_ecc's
-// verify_multiple does.
-struct VmHost {
-  std::vector<uint8_t> pks_perm;     // pks reordered by group
-  std::vector<uint32_t> offsets;     // group offsets into pks_perm
-  std::vector<uint8_t> msgs;         // distinct messages, msg_len each
+// Host plan for a batch of bls_verify_multiple calls.  Within each call the
+// pubkeys are grouped by distinct message (first-appearance order), as py_ecc's
+// verify_multiple does; every group becomes one pair
+// (hash_to_G2(m), sum of its pubkeys), and each call adds (sig, -g1).
+struct VmPlan {
+  size_t n_calls = 0, G = 0, npairs = 0;
+  std::vector<uint8_t> pks_perm;        // pubkeys reordered by group
+  std::vector<uint32_t> group_off;      // G + 1 offsets into pks_perm (in keys)
+  std::vector<uint8_t> group_msg;       // G x mlen
+  std::vector<uint8_t> group_dom;       // G x 8 (domain of the owning call)
+  std::vector<int32_t> pair_src;        // >= 0: group index; < 0: -(call + 1) = signature pair
+  std::vector<uint32_t> call_pair_off;  // n_calls + 1 offsets into pairs
+  std::vector<std::vector<agg_chunk>> passes;  // segmented Fp12 product passes
+  AggPlan agg;                                 // group pubkey sums
 };
-VmHost group_by_message(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t mlen) {
-  VmHost h;
-  std::unordered_map<std::string, uint32_t> idx;
-  std::vector<std::vector<uint32_t>> members;
-  for (size_t i = 0; i < n; ++i) {
-    std::string key((const char*)msgs + mlen * i, mlen);
-    auto it = idx.find(key);
-    uint32_t g;
-    if (it == idx.end()) {
-      g = (uint32_t)members.size();
-      idx.emplace(key, g);
-      members.emplace_back();
-      h.msgs.insert(h.msgs.end(), msgs + mlen * i, msgs + mlen * (i + 1));
-    } else {
-      g = it->second;
+
+constexpr uint32_t PROD_CHUNK = 8;
+
+// Segmented product passes over segments off[c]..off[c+1]: each pass multiplies
+// runs of <= PROD_CHUNK values; it ends when every segment is one value.  An
+// empty segment yields one chunk {b, b} (product 1).  At least one pass runs.
+std::vector<std::vector<agg_chunk>> plan_products(std::vector<uint32_t> off) {
+  std::vector<std::vector<agg_chunk>> passes;
+  const size_t ns = off.size() - 1;
+  while (true) {
+    std::vector<agg_chunk> chunks;
+    std::vector<uint32_t> next(ns + 1, 0);
+    bool more = false;
+    for (size_t c = 0; c < ns; ++c) {
+      next[c] = (uint32_t)chunks.size();
+      const uint32_t b0 = off[c], e0 = off[c + 1];
+      if (e0 <= b0) { chunks.push_back({b0, b0}); continue; }
+      for (uint32_t x = b0; x < e0; x += PROD_CHUNK) chunks.push_back({x, x + PROD_CHUNK < e0 ? x + PROD_CHUNK : e0});
+      if (e0 - b0 > PROD_CHUNK) more = true;
     }
-    members[g].push_back((uint32_t)i);
+    next[ns] = (uint32_t)chunks.size();
+    passes.push_back(std::move(chunks));
+    off = std::move(next);
+    if (!more) break;
   }
-  h.offsets.push_back(0);
-  for (auto& m : members) {
-    for (uint32_t i : m) h.pks_perm.insert(h.pks_perm.end(), pks + 48 * i, pks + 48 * (i + 1));
-    h.offsets.push_back((uint32_t)(h.pks_perm.size() / 48));
-  }
-  return h;
+  return passes;
 }
 
-// pair k < G: (H(msg_k), agg_k); pair G (if with_sig): (sig, -g1).  Statuses:
-// any BAD -> BAD; an infinite operand contributes 1.
-__global__ void __launch_bounds__(KBLOCK) k_miller_vm(size_t G, int with_sig, const uint32_t* __restrict__ h_aff,
-                                                     const uint8_t* __restrict__ h_st,
-                                                     const uint32_t* __restrict__ agg_aff,
-                                                     const uint8_t* __restrict__ agg_st,
-                                                     const uint32_t* __restrict__ sig_aff,
-                                                     const uint8_t* __restrict__ sig_st,
-                                                     uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t np = G + (with_sig ? 1 : 0);
+VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* pks, const uint8_t* msgs, size_t mlen,
+               const uint8_t* dom8s, int dom_stride, const int* with_sig) {
+  VmPlan pl;
+  pl.n_calls = n_calls;
+  pl.group_off.push_back(0);
+  pl.call_pair_off.push_back(0);
+  for (size_t c = 0; c < n_calls; ++c) {
+    std::unordered_map<std::string, uint32_t> idx;
+    std::vector<std::vector<uint32_t>> members;
+    for (uint32_t i = call_off[c]; i < call_off[c + 1]; ++i) {
+      std::string key((const char*)msgs + mlen * i, mlen);
+      auto it = idx.find(key);
+      if (it == idx.end()) {
+        idx.emplace(key, (uint32_t)members.size());
+        members.push_back({i});
+        pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * i, msgs + mlen * (i + 1));
+        pl.group_dom.insert(pl.group_dom.end(), dom8s + (size_t)dom_stride * c, dom8s + (size_t)dom_stride * c + 8);
+      } else {
+        members[it->second].push_back(i);
+      }
+    }
+    for (auto& m : members) {
+      for (uint32_t i : m) pl.pks_perm.insert(pl.pks_perm.end(), pks + 48 * (size_t)i, pks + 48 * ((size_t)i + 1));
+      pl.group_off.push_back((uint32_t)(pl.pks_perm.size() / 48));
+      pl.pair_src.push_back((int32_t)pl.G);
+      ++pl.G;
+    }
+    if (with_sig[c]) pl.pair_src.push_back(-(int32_t)c - 1);
+    pl.call_pair_off.push_back((uint32_t)pl.pair_src.size());
+  }
+  pl.npairs = pl.pair_src.size();
+  pl.passes = plan_products(pl.call_pair_off);
+  if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
+  return pl;
+}
+
+// one Miller loop per pair; statuses: any BAD operand -> BAD, an infinite operand -> 1
+__global__ void __launch_bounds__(KBLOCK) k_miller_pairs_batch(size_t npairs, const int32_t* __restrict__ src,
+                                                              size_t G, const uint32_t* __restrict__ h_aff,
+                                                              const uint8_t* __restrict__ h_st,
+                                                              const uint32_t* __restrict__ agg_aff,
+                                                              const uint8_t* __restrict__ agg_st, size_t ncalls,
+                                                              const uint32_t* __restrict__ sig_aff,
+                                                              const uint8_t* __restrict__ sig_st,
+                                                              uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
   const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= np) return;
+  if (k >= npairs) return;
+  const int32_t s = src[k];
   uint8_t sq, sp;
   aff_t<fp2_t> Q;
   aff_t<fp_t> P;
-  if (k < G) {
-    sq = h_st[k];
-    sp = agg_st[k];
-    if (sq == ST_OK && sp == ST_OK) { Q = soa_ld_g2(h_aff, G, k); P = soa_ld_g1(agg_aff, G, k); }
+  if (s >= 0) {
+    sq = h_st[s];
+    sp = agg_st[s];
+    if (sq == ST_OK && sp == ST_OK) { Q = soa_ld_g2(h_aff, G, (size_t)s); P = soa_ld_g1(agg_aff, G, (size_t)s); }
   } else {
-    sq = sig_st[0];
+    const size_t c = (size_t)(-s - 1);
+    sq = sig_st[c];
     sp = ST_OK;
-    if (sq == ST_OK) { Q = soa_ld_g2(sig_aff, 1, 0); P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M; }
+    if (sq == ST_OK) { Q = soa_ld_g2(sig_aff, ncalls, c); P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M; }
   }
   fp12_t f = fp12_one();
   uint8_t st = ST_OK;
   if (sq == ST_BAD || sp == ST_BAD) st = ST_BAD;
   else if (sq == ST_OK && sp == ST_OK) f = miller_loop_1(Q, g1_prepare(P));
-  soa_st12(f_out, np, k, f);
+  soa_st12(f_out, npairs, k, f);
   st_out[k] = st;
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_fp12_pair_product_st(size_t m, const uint32_t* __restrict__ in,
-                                                                const uint8_t* __restrict__ in_st,
-                                                                uint32_t* __restrict__ out, uint8_t* __restrict__ out_st) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t half = (m + 1) / 2;
-  if (j >= half) return;
-  fp12_t a = soa_ld12(in, m, 2 * j);
-  uint8_t st = in_st[2 * j];
-  if (2 * j + 1 < m) {
-    a = fp12_mul(a, soa_ld12(in, m, 2 * j + 1));
-    if (in_st[2 * j + 1] != ST_OK) st = ST_BAD;
+// each lane multiplies one chunk [begin, end) of Fp12 values (statuses OR-ed);
+// an empty chunk yields 1 (the empty product of an empty call)
+__global__ void __launch_bounds__(KBLOCK) k_fp12_chunk_product(size_t nchunks, const agg_chunk* __restrict__ chunks,
+                                                              const uint32_t* __restrict__ in, size_t n_in,
+                                                              const uint8_t* __restrict__ in_st,
+                                                              uint32_t* __restrict__ out, uint8_t* __restrict__ out_st) {
+  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= nchunks) return;
+  const agg_chunk ch = chunks[c];
+  fp12_t a = fp12_one();
+  uint8_t st = ST_OK;
+  for (uint32_t e = ch.begin; e < ch.end; ++e) {
+    a = (e == ch.begin) ? soa_ld12(in, n_in, e) : fp12_mul(a, soa_ld12(in, n_in, e));
+    if (in_st[e] != ST_OK) st = ST_BAD;
   }
-  soa_st12(out, half, j, a);
-  out_st[j] = st;
+  soa_st12(out, nchunks, c, a);
+  out_st[c] = st;
 }
 
-// reduce m Fp12 (+status) to one by pairwise product passes; returns final buffers
-int reduce_fp12(size_t m, uint32_t* f, uint8_t* st, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st) {
-  while (m > 1) {
-    const size_t half = (m + 1) / 2;
-    uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * half);
-    uint8_t* nst = b.take<uint8_t>(half);
-    LAUNCH("fp12_product", s, dim3(grid_for(half)), dim3(KBLOCK), k_fp12_pair_product_st, m, (const uint32_t*)f,
-           (const uint8_t*)st, nf, nst);
+// Runs a planned batch up to (and excluding) the final exponentiation.  Returns
+// per-call Fp12 products and statuses (SoA over n_calls) on the device.
+int run_vm_batch(const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hipStream_t s, uint32_t** out_f,
+                 uint8_t** out_st) {
+  const size_t G = pl.G, ncalls = pl.n_calls, np = pl.npairs;
+  uint8_t* d_pks = b.take<uint8_t>(pl.pks_perm.size() + 1);
+  uint8_t* d_msgs = b.take<uint8_t>(pl.group_msg.size() + 1);
+  uint8_t* d_doms = b.take<uint8_t>(pl.group_dom.size() + 1);
+  uint8_t* d_sigs = b.take<uint8_t>(96 * ncalls);
+  int32_t* d_src = b.take<int32_t>(np + 1);
+  if (!pl.pks_perm.empty()) HIPC(hipMemcpyAsync(d_pks, pl.pks_perm.data(), pl.pks_perm.size(), hipMemcpyHostToDevice, s));
+  if (!pl.group_msg.empty()) HIPC(hipMemcpyAsync(d_msgs, pl.group_msg.data(), pl.group_msg.size(), hipMemcpyHostToDevice, s));
+  if (!pl.group_dom.empty()) HIPC(hipMemcpyAsync(d_doms, pl.group_dom.data(), pl.group_dom.size(), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * ncalls, hipMemcpyHostToDevice, s));
+  if (np) HIPC(hipMemcpyAsync(d_src, pl.pair_src.data(), np * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  // group sums -> affine + subgroup check
+  uint32_t* agg_aff = b.take<uint32_t>(2 * FP_LIMBS * (G + 1));
+  uint8_t* agg_st = b.take<uint8_t>(G + 1);
+  uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
+  uint8_t* h_st = b.take<uint8_t>(G + 1);
+  if (G > 0) {
+    const uint32_t* jac;
+    const uint8_t* bad;
+    size_t used = 0;
+    uint8_t* sub = b.take<uint8_t>(0);
+    int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, s, &jac, &bad, &used, b.left());
+    if (rc) return rc;
+    b.off += used;
+    LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
+    LAUNCH("hash_to_g2", s, dim3(grid_for(G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
+           (const uint8_t*)d_doms, 8, h_aff, h_st);
+  }
+  uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
+  uint8_t* sig_st = b.take<uint8_t>(ncalls);
+  LAUNCH("decode_g2", s, dim3(grid_for(ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs, sig_aff,
+         sig_st, 1);
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * (np + 1));
+  uint8_t* st = b.take<uint8_t>(np + 1);
+  if (np)
+    LAUNCH("miller_loop_1", s, dim3(grid_for(np)), dim3(KBLOCK), k_miller_pairs_batch, np, (const int32_t*)d_src, G,
+           (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+  // segmented products (chunk lists live in the plan, which outlives the stream work)
+  size_t n_in = np;
+  for (const auto& chunks : pl.passes) {
+    agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
+    uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
+    uint8_t* nst = b.take<uint8_t>(chunks.size());
+    HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+    LAUNCH("fp12_product", s, dim3(grid_for(chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
+           (const agg_chunk*)d_ch, (const uint32_t*)f, n_in, (const uint8_t*)st, nf, nst);
     f = nf;
     st = nst;
-    m = half;
+    n_in = chunks.size();
   }
   *out_f = f;
   *out_st = st;
   return 0;
 }
 
-// Everything of a verify_multiple call up to (and excluding) the final
-// exponentiation.  Leaves the single Fp12 product and its status on device.
-int vm_partial(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, size_t mlen, const uint8_t* sig,
-               int with_sig, const uint8_t* dom8, uint32_t** d_f, uint8_t** d_st, Bump& b) {
-  hipStream_t s = c->stream;
-  VmHost h = group_by_message(n, pks, msgs, mlen);
-  const size_t G = h.offsets.size() - 1;
-  AggPlan plan = plan_agg(G, h.offsets.data());
-  // inputs
-  uint8_t* d_pks = b.take<uint8_t>(h.pks_perm.size() + 1);
-  uint8_t* d_msgs = b.take<uint8_t>(h.msgs.size() + 1);
-  uint8_t* d_sig = b.take<uint8_t>(96);
-  uint8_t* d_dom = b.take<uint8_t>(8);
-  if (!h.pks_perm.empty()) HIPC(hipMemcpyAsync(d_pks, h.pks_perm.data(), h.pks_perm.size(), hipMemcpyHostToDevice, s));
-  if (!h.msgs.empty()) HIPC(hipMemcpyAsync(d_msgs, h.msgs.data(), h.msgs.size(), hipMemcpyHostToDevice, s));
-  HIPC(hipMemcpyAsync(d_sig, sig, 96, hipMemcpyHostToDevice, s));
-  HIPC(hipMemcpyAsync(d_dom, dom8, 8, hipMemcpyHostToDevice, s));
-  // group sums -> affine + subgroup check
-  uint32_t* agg_aff = b.take<uint32_t>(2 * FP_LIMBS * (G + 1));
-  uint8_t* agg_st = b.take<uint8_t>(G + 1);
-  if (G > 0) {
-    const uint32_t* jac;
-    const uint8_t* bad;
-    size_t used = 0;
-    uint8_t* sub = b.take<uint8_t>(0);
-    int rc = run_agg<fp_t>(plan, G, d_pks, sub, s, &jac, &bad, &used);
-    if (rc) return rc;
-    b.off += used;
-    LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
-  }
-  // hashes of distinct messages
-  uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
-  uint8_t* h_st = b.take<uint8_t>(G + 1);
-  if (G > 0)
-    LAUNCH("hash_to_g2", s, dim3(grid_for(G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
-           (const uint8_t*)d_dom, 0, h_aff, h_st);
-  // signature
-  uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS);
-  uint8_t* sig_st = b.take<uint8_t>(1);
-  LAUNCH("decode_g2", s, dim3(1), dim3(KBLOCK), k_decode_g2, (size_t)1, (const uint8_t*)d_sig, sig_aff, sig_st, 1);
-  const size_t np = G + (with_sig ? 1 : 0);
-  if (np == 0) {
-    // empty product: f = 1 (py_ecc's FQ12.one() start value)
-    uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS);
-    uint8_t* st = b.take<uint8_t>(1);
-    std::vector<uint8_t> one(576, 0);
-    one[47] = 1;
-    uint8_t* tmp = b.take<uint8_t>(576);
-    HIPC(hipMemcpyAsync(tmp, one.data(), 576, hipMemcpyHostToDevice, s));
-    LAUNCH("fp12_from_bytes", s, dim3(1), dim3(KBLOCK), k_fp12_from_bytes, (size_t)1, (const uint8_t*)tmp, f);
-    HIPC(hipMemsetAsync(st, 0, 1, s));
-    // the host vector must outlive the async copy
-    HIPC(hipStreamSynchronize(s));
-    *d_f = f;
-    *d_st = st;
-    return 0;
-  }
-  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * np);
-  uint8_t* st = b.take<uint8_t>(np);
-  LAUNCH("miller_loop_1", s, dim3(grid_for(np)), dim3(KBLOCK), k_miller_vm, G, with_sig, (const uint32_t*)h_aff,
-         (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, (const uint32_t*)sig_aff,
-         (const uint8_t*)sig_st, f, st);
-  return reduce_fp12(np, f, st, b, s, d_f, d_st);
-}
-
-size_t vm_ws_bound(size_t n, size_t mlen) {
-  // generous bound: inputs + per-group buffers + agg levels + Miller tree
-  const size_t G = n + 1;
-  return 4096 + align256(48 * n) + align256(mlen * n) + 2 * 1024 +
-         align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G) + 1024 +
-         3 * (align256(12 * FPW * G) + align256(G)) + 2 * (align256(G * 12) + align256(G * 3 * FPW) + align256(G)) +
-         (size_t)(2 * G / (CHUNK_L1) + 64) * (3 * FPW + 16);
+size_t vm_ws_bound(const VmPlan& pl, size_t mlen) {
+  const size_t G = pl.G + 1, np = pl.npairs + 1, nc = pl.n_calls + 1;
+  size_t s = 1 << 16;
+  s += align256(pl.pks_perm.size() + 1) + align256(G * mlen + 1) + align256(G * 8 + 1) + align256(96 * nc) +
+       align256(4 * np);
+  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
+  s += agg_ws_size(pl.agg, 3) + 256;
+  s += align256(4 * FPW * nc) + align256(nc);
+  s += align256(12 * FPW * np) + align256(np);
+  for (const auto& ch : pl.passes)
+    s += align256(ch.size() * sizeof(agg_chunk)) + align256(12 * FPW * ch.size()) + align256(ch.size());
+  s += align256(nc);
+  return s;
 }
 
 }  // namespace
@@ -448,6 +518,9 @@ void bls381_shutdown(void) {
     if (!c) continue;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)hipDeviceSynchronize();
+    for (auto& k : c->keep) (void)hipEventDestroy(k.ev);
+    c->keep.clear();
     if (c->ws) (void)hipFree(c->ws);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -508,7 +581,7 @@ int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_
 }
 
 int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
-                        const uint8_t* dom8s, uint8_t* verdicts_out) {
+                        const uint8_t* dom8s, uint8_t* verdicts_out) try {
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
@@ -517,7 +590,7 @@ int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, con
   std::lock_guard<std::mutex> lk(c->mu);
   const size_t in_bytes = align256(48 * n) + align256(32 * n) + align256(96 * n) + align256(8 * n) + align256(n);
   if ((rc = ensure_ws(c, in_bytes + verify_ws_size(n) + 1024))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_pks = b.take<uint8_t>(48 * n);
   uint8_t* d_msgs = b.take<uint8_t>(32 * n);
   uint8_t* d_sigs = b.take<uint8_t>(96 * n);
@@ -533,6 +606,9 @@ int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, con
   HIPC(hipMemcpyAsync(verdicts_out, d_v, n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
 int bls381_verify(const uint8_t pk[48], const uint8_t* msg, size_t msg_len, const uint8_t sig[96],
@@ -548,39 +624,58 @@ int bls381_verify(const uint8_t pk[48], const uint8_t* msg, size_t msg_len, cons
   return bls381_verify_multiple(1, pk, msg, msg_len, sig, dom8);
 }
 
-int bls381_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len, const uint8_t sig[96],
-                           const uint8_t dom8[8]) {
-  if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
+                                 const uint8_t* msgs, size_t msg_len, const uint8_t* sigs, const uint8_t* dom8s,
+                                 uint8_t* verdicts) try {
+  if (n_calls == 0) return 0;
+  if (!call_off || !sigs || !dom8s || !verdicts || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  if (call_off[n_calls] && (!pks || (!msgs && msg_len))) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  if ((rc = ensure_ws(c, vm_ws_bound(n, msg_len)))) return rc;
-  Bump b(c->ws);
+  std::vector<int> with_sig(n_calls, 1);
+  VmPlan pl = plan_vm(n_calls, call_off, pks, msgs, msg_len, dom8s, 8, with_sig.data());
+  if ((rc = ensure_ws(c, vm_ws_bound(pl, msg_len)))) return rc;
+  Bump b(c->ws, c->ws_cap);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = vm_partial(c, n, pks, msgs, msg_len, sig, 1, dom8, &f, &st, b))) return rc;
-  uint8_t* d_v = b.take<uint8_t>(1);
-  LAUNCH("final_exp", c->stream, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)f,
-         (const uint8_t*)st, d_v);
-  uint8_t v = 0;
-  HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, c->stream));
+  if ((rc = run_vm_batch(pl, msg_len, sigs, b, c->stream, &f, &st))) return rc;
+  uint8_t* d_v = b.take<uint8_t>(n_calls);
+  LAUNCH("final_exp", c->stream, dim3(grid_for(n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
+         (const uint32_t*)f, (const uint8_t*)st, d_v);
+  HIPC(hipMemcpyAsync(verdicts, d_v, n_calls, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
-  return v;
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len, const uint8_t sig[96],
+                           const uint8_t dom8[8]) {
+  if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  const uint32_t off[2] = {0, (uint32_t)n};
+  uint8_t v = 0;
+  const int rc = bls381_verify_multiple_batch(1, off, pks, msgs, msg_len, sig, dom8, &v);
+  return rc ? rc : v;
 }
 
 int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len, const uint8_t sig[96],
-                          int include_sig, const uint8_t dom8[8], uint8_t out576[576]) {
+                          int include_sig, const uint8_t dom8[8], uint8_t out576[576]) try {
   if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || !out576 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  if ((rc = ensure_ws(c, vm_ws_bound(n, msg_len)))) return rc;
-  Bump b(c->ws);
+  const uint32_t off[2] = {0, (uint32_t)n};
+  const int with_sig = include_sig ? 1 : 0;
+  VmPlan pl = plan_vm(1, off, pks, msgs, msg_len, dom8, 8, &with_sig);
+  if ((rc = ensure_ws(c, vm_ws_bound(pl, msg_len)))) return rc;
+  Bump b(c->ws, c->ws_cap);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = vm_partial(c, n, pks, msgs, msg_len, sig, include_sig ? 1 : 0, dom8, &f, &st, b))) return rc;
+  if ((rc = run_vm_batch(pl, msg_len, sig, b, c->stream, &f, &st))) return rc;
   uint8_t* d_out = b.take<uint8_t>(576);
   LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(64), k_fp12_to_bytes, (const uint32_t*)f, (size_t)1, (size_t)0,
          d_out);
@@ -589,16 +684,19 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
   HIPC(hipMemcpyAsync(&h_st, st, 1, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   return h_st == ST_OK ? 0 : 1;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-int bls381_final_verify(size_t k, const uint8_t* parts576) {
+int bls381_final_verify(size_t k, const uint8_t* parts576) try {
   if (k == 0 || !parts576) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
-  if ((rc = ensure_ws(c, 4 * (align256(576 * k) + align256(12 * FPW * k) + align256(k)) + 8192))) return rc;
-  Bump b(c->ws);
+  if ((rc = ensure_ws(c, 4 * (align256(576 * k) + align256(12 * FPW * k) + align256(k) + 1024) + 8192))) return rc;
+  Bump b(c->ws, c->ws_cap);
   hipStream_t s = c->stream;
   uint8_t* d_in = b.take<uint8_t>(576 * k);
   uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * k);
@@ -606,22 +704,37 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) {
   HIPC(hipMemcpyAsync(d_in, parts576, 576 * k, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(st, 0, k, s));
   LAUNCH("fp12_from_bytes", s, dim3(grid_for(k)), dim3(KBLOCK), k_fp12_from_bytes, k, (const uint8_t*)d_in, f);
-  uint32_t* rf;
-  uint8_t* rst;
-  if ((rc = reduce_fp12(k, f, st, b, s, &rf, &rst))) return rc;
+  const auto passes = plan_products({0u, (uint32_t)k});
+  size_t n_in = k;
+  for (const auto& chunks : passes) {
+    agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
+    uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
+    uint8_t* nst = b.take<uint8_t>(chunks.size());
+    HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+    LAUNCH("fp12_product", s, dim3(grid_for(chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
+           (const agg_chunk*)d_ch, (const uint32_t*)f, n_in, (const uint8_t*)st, nf, nst);
+    f = nf;
+    st = nst;
+    n_in = chunks.size();
+  }
   uint8_t* d_v = b.take<uint8_t>(1);
-  LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)rf,
-         (const uint8_t*)rst, d_v);
+  LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)f,
+         (const uint8_t*)st, d_v);
   uint8_t v = 0;
   HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return v;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
 // ---- aggregation
-static int agg_batch_impl(int is_g2, size_t ng, const uint32_t* offsets, size_t n_pts, const uint8_t* d_pts,
+static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets, size_t n_pts, const uint8_t* d_pts,
                           uint8_t* d_out, int32_t* d_status, void* ws, hipStream_t s) {
-  AggPlan plan = plan_agg(ng, offsets);
+  // the chunk lists are async-copy sources: they live until the stream passes them
+  auto hold = std::make_shared<AggPlan>(plan_agg(ng, offsets));
+  const AggPlan& plan = *hold;
   const uint32_t* jac;
   const uint8_t* bad;
   size_t used = 0;
@@ -634,7 +747,7 @@ static int agg_batch_impl(int is_g2, size_t ng, const uint32_t* offsets, size_t 
     if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
   }
-  return 0;
+  return keep_until_done(c, s, hold);
 }
 
 static size_t agg_ws_bytes(int is_g2, size_t ng, const uint32_t* offsets) {
@@ -657,7 +770,7 @@ int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_off
   if (n_groups == 0) return 0;
   if (!h_offsets || !d_out48 || !d_status || !d_workspace) return BLS381_EARG;
   hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-  return agg_batch_impl(0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace, s);
+  return agg_batch_impl(c, 0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace, s);
 }
 
 static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t* pts, uint8_t* out, int32_t* status) {
@@ -669,13 +782,13 @@ static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t
   const size_t npts = offsets[ng];
   const size_t need = align256(npts * bytes + 1) + align256(ng * bytes) + align256(ng * 4) + agg_ws_bytes(is_g2, ng, offsets) + 4096;
   if ((rc = ensure_ws(c, need))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_pts = b.take<uint8_t>(npts * bytes + 1);
   uint8_t* d_out = b.take<uint8_t>(ng * bytes);
   int32_t* d_st = b.take<int32_t>(ng);
   hipStream_t s = c->stream;
   if (npts) HIPC(hipMemcpyAsync(d_pts, pts, npts * bytes, hipMemcpyHostToDevice, s));
-  if ((rc = agg_batch_impl(is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off), s))) return rc;
+  if ((rc = agg_batch_impl(c, is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off), s))) return rc;
   HIPC(hipMemcpyAsync(out, d_out, ng * bytes, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(status, d_st, ng * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -706,14 +819,14 @@ int bls381_aggregate_signatures(size_t n, const uint8_t* sigs, uint8_t out[96]) 
 }
 
 // ---- single-item helpers (fixtures / reference API)
-int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const uint8_t dom8[8], uint8_t out[96]) {
+int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const uint8_t dom8[8], uint8_t out[96]) try {
   if ((!msg && msg_len) || !sk || !dom8 || !out || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure_ws(c, 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_msg = b.take<uint8_t>(msg_len + 1);
   uint8_t* d_sk = b.take<uint8_t>(32);
   uint8_t* d_dom = b.take<uint8_t>(8);
@@ -727,9 +840,12 @@ int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const 
   HIPC(hipMemcpyAsync(out, d_out, 96, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const uint8_t* dom8s, uint8_t* out96) {
+int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const uint8_t* dom8s, uint8_t* out96) try {
   if (n == 0) return 0;
   if (!msgs32 || !sks || !dom8s || !out96) return BLS381_EARG;
   int rc = 0;
@@ -737,7 +853,7 @@ int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure_ws(c, align256(32 * n) * 2 + align256(8 * n) + align256(96 * n) + 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_msg = b.take<uint8_t>(32 * n);
   uint8_t* d_sk = b.take<uint8_t>(32 * n);
   uint8_t* d_dom = b.take<uint8_t>(8 * n);
@@ -751,9 +867,12 @@ int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const
   HIPC(hipMemcpyAsync(out96, d_out, 96 * n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48) {
+int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48) try {
   if (n == 0) return 0;
   if (!sks || !out48) return BLS381_EARG;
   int rc = 0;
@@ -761,7 +880,7 @@ int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48) {
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure_ws(c, align256(32 * n) + align256(48 * n) + 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_sk = b.take<uint8_t>(32 * n);
   uint8_t* d_out = b.take<uint8_t>(48 * n);
   hipStream_t s = c->stream;
@@ -770,16 +889,19 @@ int bls381_privtopub_batch(size_t n, const uint8_t* sks, uint8_t* out48) {
   HIPC(hipMemcpyAsync(out48, d_out, 48 * n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-int bls381_privtopub(const uint8_t sk[32], uint8_t out[48]) {
+int bls381_privtopub(const uint8_t sk[32], uint8_t out[48]) try {
   if (!sk || !out) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure_ws(c, 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_sk = b.take<uint8_t>(32);
   uint8_t* d_out = b.take<uint8_t>(48);
   hipStream_t s = c->stream;
@@ -788,17 +910,20 @@ int bls381_privtopub(const uint8_t sk[32], uint8_t out[48]) {
   HIPC(hipMemcpyAsync(out, d_out, 48, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
 int bls381_hash_to_g2(const uint8_t* msg, size_t msg_len, const uint8_t dom8[8], uint8_t out_compressed[96],
-                      uint8_t out_affine[192]) {
+                      uint8_t out_affine[192]) try {
   if ((!msg && msg_len) || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   if ((rc = ensure_ws(c, 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_msg = b.take<uint8_t>(msg_len + 1);
   uint8_t* d_dom = b.take<uint8_t>(8);
   uint8_t* d_comp = b.take<uint8_t>(96);
@@ -812,9 +937,12 @@ int bls381_hash_to_g2(const uint8_t* msg, size_t msg_len, const uint8_t dom8[8],
   if (out_affine) HIPC(hipMemcpyAsync(out_affine, d_aff, 192, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const uint8_t* dom8s, uint8_t* out288) {
+int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const uint8_t* dom8s, uint8_t* out288) try {
   if (n == 0) return 0;
   if (!msgs32 || !dom8s || !out288) return BLS381_EARG;
   int rc = 0;
@@ -823,7 +951,7 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
   std::lock_guard<std::mutex> lk(c->mu);
   const size_t scratch = (size_t)n * H2_BITS * 6 * FPW;
   if ((rc = ensure_ws(c, align256(32 * n) + align256(8 * n) + align256(288 * n) + align256(scratch) + 4096))) return rc;
-  Bump b(c->ws);
+  Bump b(c->ws, c->ws_cap);
   uint8_t* d_msgs = b.take<uint8_t>(32 * n);
   uint8_t* d_doms = b.take<uint8_t>(8 * n);
   uint8_t* d_out = b.take<uint8_t>(288 * n);
@@ -836,6 +964,9 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
   HIPC(hipMemcpyAsync(out288, d_out, 288 * n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
 }  // extern "C"

@@ -561,7 +561,7 @@ BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2
 // Fp4[w]/(w^3 - z), Fp4 = Fp2[z]/(z^2 - xi), z = w^3:
 //   f = A + B w + C w^2,  A = a0 + b1 z,  B = b0 + a2 z,  C = a1 + b2 z
 //   A' = 3A^2 - 2 conj(A),  B' = 3 z C^2 + 2 conj(B),  C' = 3 B^2 - 2 conj(C)
-BLS_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
+BLS_INLINE fp12_t fp12_cyclotomic_sqr_inl(const fp12_t& f) {
   const fp2_t& a0 = f.c0.c0; const fp2_t& a1 = f.c0.c1; const fp2_t& a2 = f.c0.c2;
   const fp2_t& b0 = f.c1.c0; const fp2_t& b1 = f.c1.c1; const fp2_t& b2 = f.c1.c2;
   auto sq4 = [](const fp2_t& x0, const fp2_t& x1, fp2_t& r0, fp2_t& r1) {
@@ -586,5 +586,8 @@ BLS_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) {
   r.c1.c2 = fp2_add(fp2_mul_small(B1, 3), fp2_dbl(b2));
   return r;
 }
+
+
+BLS_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) { return fp12_cyclotomic_sqr_inl(f); }
 
 }  // namespace bls381

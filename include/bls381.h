@@ -118,6 +118,13 @@ int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_off
                                           const uint8_t* d_pks, uint8_t* d_out48, int32_t* d_status,
                                           void* d_workspace, void* stream);
 
+/* n_calls independent bls_verify_multiple calls: call c
+ * owns pubkeys/messages [call_off[c], call_off[c+1]) (host offsets, n_calls+1
+ * entries), signature sigs[c] (96 B) and dom8s[c] (8 B).  verdicts[c] = 1/0. */
+int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
+                                 const uint8_t* msgs, size_t msg_len, const uint8_t* sigs, const uint8_t* dom8s,
+                                 uint8_t* verdicts);
+
 /* ---- multi-GPU partial products --------------------------- */
 /* Miller-loop product of one shard of a bls_verify_multiple call: pairs
  * (hash_to_G2(msg_g), group_pubkey_g) for the messages in this shard, plus

@@ -263,3 +263,131 @@ def test_deterministic_replay(native):
     a = native.verify_batch(*args)
     b = native.verify_batch(*args)
     assert (a == b).all() and list(a) == exp
+
+
+# ---------------------------------- batched bls_verify_multiple (C3 / C5 shapes)
+def test_verify_multiple_batch_golden(native, golden):
+    """All golden verify_multiple cases as ONE batch: per-call verdicts == py_ecc's."""
+    _, gb = golden
+    cases = [c for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+    off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+    for c in cases:
+        pks += b"".join(bytes.fromhex(p) for p in c["pubkeys"])
+        msgs += b"".join(bytes.fromhex(m) for m in c["messages"])
+        sigs += bytes.fromhex(c["signature"])
+        doms += int(c["domain"]).to_bytes(8, "big")
+        off.append(off[-1] + len(c["pubkeys"]))
+    v = native.verify_multiple_batch(off, pks, msgs, 32, sigs, doms)
+    assert list(v) == [c["expected"] for c in cases]
+
+
+def _committee_calls(rng, n_calls, max_keys, sks):
+    """Calls of 0..max_keys members over 1..3 distinct messages, signed with the engine."""
+    from bls381_amd import bls
+    calls = []
+    for c in range(n_calls):
+        k = rng.randrange(0, max_keys + 1)
+        members = [rng.randrange(len(sks)) for _ in range(k)]
+        cand = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(rng.randrange(1, 4))]
+        msgs = [cand[rng.randrange(len(cand))] for _ in range(k)]
+        dom = rng.getrandbits(64)
+        sig = bls.bls_aggregate_signatures([bls.bls_sign(m, sks[i], dom) for i, m in zip(members, msgs)])
+        calls.append([members, msgs, sig, dom, True])
+    return calls
+
+
+def test_verify_multiple_batch_committees(native):
+    """C3 shape: many calls, ragged sizes (incl. empty), tampered calls; == single-call API."""
+    from bls381_amd import bls
+    rng = random.Random(0xB15_0C03)
+    sks = [rng.randrange(1, O.r) for _ in range(24)]
+    pubs = [bls.privtopub(k) for k in sks]
+    calls = _committee_calls(rng, 40, 12, sks)
+    for j, cl in enumerate(calls):
+        if j % 5 == 1:                     # other call's signature
+            cl[2] = calls[j - 1][2]
+            cl[4] = len(cl[0]) == 0 and len(calls[j - 1][0]) == 0
+        elif j % 5 == 2:                   # wrong domain
+            cl[3] ^= 1
+            cl[4] = len(cl[0]) == 0
+        elif j % 5 == 3 and cl[0]:         # one member swapped for another key
+            cl[0] = [(cl[0][0] + 1) % len(sks)] + cl[0][1:]
+            cl[4] = False
+    off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+    for members, ms, sig, dom, _ in calls:
+        pks += b"".join(pubs[i] for i in members)
+        msgs += b"".join(ms)
+        sigs += sig
+        doms += dom.to_bytes(8, "big")
+        off.append(off[-1] + len(members))
+    v = native.verify_multiple_batch(off, pks, msgs, 32, sigs, doms)
+    single = [bls.bls_verify_multiple([pubs[i] for i in m], ms, s, d) for m, ms, s, d, _ in calls]
+    assert list(v) == single
+    assert list(v) == [c[4] for c in calls]
+
+
+def test_verify_multiple_batch_many_messages(native):
+    """C5 shape: calls with 70 and 9 distinct messages (multi-pass segmented product) beside small ones."""
+    from bls381_amd import bls
+    rng = random.Random(0xB15_0C05)
+    calls = []
+    for L in (70, 1, 9, 8, 2):
+        sks = [rng.randrange(1, O.r) for _ in range(L)]
+        ms = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(L)]
+        pks = native.privtopub_batch(b"".join(k.to_bytes(32, "big") for k in sks))
+        sig = bls.bls_aggregate_signatures(
+            [native.sign_batch(b"".join(ms), b"".join(k.to_bytes(32, "big") for k in sks),
+                               (5).to_bytes(8, "big") * L)[96 * i:96 * i + 96] for i in range(L)])
+        calls.append((pks, b"".join(ms), sig))
+    off = np.cumsum([0] + [len(p) // 48 for p, _, _ in calls])
+    good = native.verify_multiple_batch(off, b"".join(p for p, _, _ in calls), b"".join(m for _, m, _ in calls), 32,
+                                        b"".join(s for _, _, s in calls), (5).to_bytes(8, "big") * len(calls))
+    assert list(good) == [True] * len(calls)
+    # rotate signatures between calls: every call fails
+    sigs = [s for _, _, s in calls]
+    sigs = sigs[1:] + sigs[:1]
+    bad = native.verify_multiple_batch(off, b"".join(p for p, _, _ in calls), b"".join(m for _, m, _ in calls), 32,
+                                       b"".join(sigs), (5).to_bytes(8, "big") * len(calls))
+    assert not bad.any()
+
+
+def test_aggregate_batch_device_async_back_to_back(native):
+    """Device-pointer aggregation returns before its copies run: two different plans queued
+    back to back on one stream, with host churn in between, must both land intact."""
+    import ctypes
+    import torch
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    keys = [O.privtopub(k) for k in range(1, 33)]
+    stream = torch.cuda.current_stream(dev)
+    runs = []
+    for ng, cs in ((2048, 3), (700, 5)):
+        # groups alternate: cs keys, then an empty group
+        sizes = [cs if g % 2 == 0 else 0 for g in range(ng)]
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+        idx = [(g * 7 + j) % 32 for g in range(ng) for j in range(sizes[g])]
+        d_pks = torch.frombuffer(bytearray(b"".join(keys[i] for i in idx)), dtype=torch.uint8).to(dev)
+        d_out = torch.zeros(ng * 48, dtype=torch.uint8, device=dev)
+        d_st = torch.full((ng,), -7, dtype=torch.int32, device=dev)
+        ws = torch.empty(L.bls381_aggregate_pubkeys_batch_workspace_size(ng, len(idx)), dtype=torch.uint8,
+                         device=dev)
+        native.check(L.bls381_aggregate_pubkeys_batch_device(
+            ng, offs.ctypes.data_as(ctypes.c_void_p), len(idx), d_pks.data_ptr(), d_out.data_ptr(), d_st.data_ptr(),
+            ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        del offs                                      # the caller's offsets may die right away
+        _ = [bytearray(1 << 16) for _ in range(64)]   # host allocation churn
+        runs.append((ng, sizes, idx, d_out, d_st, d_pks, ws))
+    torch.cuda.synchronize()
+    cache = {}
+    for ng, sizes, idx, d_out, d_st, _, _ in runs:
+        assert int(d_st.abs().sum().item()) == 0
+        out = d_out.cpu().numpy().tobytes()
+        pos = 0
+        for g in range(ng):
+            members = idx[pos:pos + sizes[g]]
+            pos += sizes[g]
+            k = sum(i + 1 for i in members)
+            if k not in cache:
+                cache[k] = O.privtopub(k) if k else bytes([0xC0]) + bytes(47)
+            want = cache[k]
+            assert out[48 * g:48 * g + 48] == want, (ng, g)

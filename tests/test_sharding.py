@@ -61,25 +61,50 @@ def model_final(parts):
     return M.final_exp(f) == M.ONE12
 
 
-def _worker(rank, world, port, case, q):
+def model_batch(call_off, pks, msgs, mlen, sigs, dom8s):
+    """CPU stand-in for bls381_verify_multiple_batch: the oracle, call by call."""
+    import bls_oracle as O
+    out = []
+    for c in range(len(call_off) - 1):
+        a, b = call_off[c], call_off[c + 1]
+        out.append(O.verify_multiple([pks[48 * i:48 * i + 48] for i in range(a, b)],
+                                     [msgs[mlen * i:mlen * i + mlen] for i in range(a, b)],
+                                     sigs[96 * c:96 * c + 96], int.from_bytes(dom8s[8 * c:8 * c + 8], "big")))
+    return out
+
+
+def _oracle_agg(pks):
+    import bls_oracle as O
+    return O.aggregate_pubkeys([pks[48 * i:48 * i + 48] for i in range(len(pks) // 48)])
+
+
+def _worker(rank, world, port, case, q, kind="vm"):
     sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch.distributed as dist
     from bls381_amd import sharding
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
-    pks, msgs, sig, dom = case
-    v = sharding.sharded_verify_multiple(pks, msgs, sig, dom, rank=rank, world=world,
-                                         partial_fn=model_partial, final_fn=model_final)
+    if kind == "vm":
+        pks, msgs, sig, dom = case
+        v = sharding.sharded_verify_multiple(pks, msgs, sig, dom, rank=rank, world=world,
+                                             partial_fn=model_partial, final_fn=model_final)
+    elif kind == "agg":
+        try:
+            v = sharding.sharded_aggregate_pubkeys(case, rank=rank, world=world, agg_fn=_oracle_agg)
+        except ValueError:
+            v = "ValueError"
+    else:
+        v = sharding.sharded_verify_multiple_batch(case, rank=rank, world=world, batch_fn=model_batch)
     q.put((rank, v))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run(case, world=2):
+def _run(case, world=2, kind="vm"):
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, case, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -118,3 +143,45 @@ def test_sharded_verify_multiple_gloo_world2(case):
     bad = (pks[::-1], msgs, sig, dom)
     res = _run(bad)
     assert res == {0: False, 1: False}
+
+
+def test_shard_range_covers_everything():
+    from bls381_amd.sharding import shard_range
+    for n in (0, 1, 5, 8, 1 << 20):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(n, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[r][1] == rs[r + 1][0] for r in range(world - 1))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+def test_sharded_aggregate_pubkeys_gloo_world2():
+    """C4 protocol: per-rank compressed partials, summed on rank 0 == one aggregate over all keys."""
+    import bls_oracle as O
+    keys = [O.privtopub(k) for k in range(1, 8)]
+    res = _run(keys, kind="agg")
+    want = O.privtopub(sum(range(1, 8)))
+    assert res == {0: want, 1: want}
+    # an invalid encoding on rank 1's half raises on both ranks
+    res = _run(keys[:6] + [b"\x01" * 48], kind="agg")
+    assert res == {0: "ValueError", 1: "ValueError"}
+    # fewer keys than ranks: the empty shard contributes infinity
+    res = _run(keys[:1], kind="agg")
+    assert res == {0: keys[0], 1: keys[0]}
+
+
+def test_sharded_verify_multiple_batch_gloo_world2(case):
+    """C4 second half: independent calls sharded by call; every rank gets all verdicts in order."""
+    import bls_oracle as O
+    pks, msgs, sig, dom = case
+    inf_sig = O.aggregate_signatures([])
+    calls = [
+        (pks[:1], msgs[:1], O.sign(msgs[0], 11, 5), 5),        # True
+        ([], [], inf_sig, 7),                                   # True (empty product)
+        (pks[:1], msgs[:1], O.sign(msgs[0], 11, 5), 6),        # wrong domain
+        ([], [], O.sign(msgs[0], 11, 5), 7),                    # empty call, non-infinite signature
+        (pks[:1], [b"\x01" * 31], O.sign(msgs[0], 11, 5), 5),  # other message length
+    ]
+    want = [True, True, False, False, False]
+    res = _run(calls, kind="batch")
+    assert res == {0: want, 1: want}
