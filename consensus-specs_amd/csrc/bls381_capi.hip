@@ -576,7 +576,7 @@ int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_
   if (!c) return rc;
   if (n == 0) return 0;
   if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace) return BLS381_EARG;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream (torch's default stream)
   return run_verify_batch(n, d_pks, d_msgs32, d_sigs, d_dom8s, d_verdicts, d_workspace, s);
 }
 
@@ -769,7 +769,7 @@ int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_off
   if (!c) return rc;
   if (n_groups == 0) return 0;
   if (!h_offsets || !d_out48 || !d_status || !d_workspace) return BLS381_EARG;
-  hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+  hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream (torch's default stream)
   return agg_batch_impl(c, 0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace, s);
 }
 

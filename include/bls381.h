@@ -100,7 +100,8 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
 int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
                         const uint8_t* dom8s, uint8_t* verdicts_out);
 
-/* Device-resident variant: all pointers are device memory, stream = hipStream_t.
+/* Device-resident variant: all pointers are device memory, stream = hipStream_t
+ * (NULL = the HIP null stream, i.e. torch's default stream; work is queued, not synchronised).
  * `workspace` must hold bls381_verify_batch_workspace_size(n) bytes. */
 size_t bls381_verify_batch_workspace_size(size_t n);
 int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32,

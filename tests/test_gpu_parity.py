@@ -391,3 +391,43 @@ def test_aggregate_batch_device_async_back_to_back(native):
                 cache[k] = O.privtopub(k) if k else bytes([0xC0]) + bytes(47)
             want = cache[k]
             assert out[48 * g:48 * g + 48] == want, (ng, g)
+
+
+def test_device_entry_points_order_on_torch_default_stream(native):
+    """stream=NULL (torch's default stream) means the HIP null stream: a torch read of the
+    output right after the call (no device-wide synchronize) must see the finished result."""
+    import ctypes
+    import torch
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    keys = [O.privtopub(k) for k in range(1, 17)]
+    ng = 512
+    sizes = [128 if g % 2 == 0 else 0 for g in range(ng)]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    idx = [(g * 5 + j) % 16 for g in range(ng) for j in range(sizes[g])]
+    host_pks = b"".join(keys[i] for i in idx)
+    d_pks = torch.frombuffer(bytearray(host_pks), dtype=torch.uint8).to(dev)
+    d_out = torch.zeros(ng * 48, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(ng, dtype=torch.int32, device=dev)
+    ws = torch.empty(L.bls381_aggregate_pubkeys_batch_workspace_size(ng, len(idx)), dtype=torch.uint8, device=dev)
+    native.check(L.bls381_aggregate_pubkeys_batch_device(
+        ng, offs.ctypes.data_as(ctypes.c_void_p), len(idx), d_pks.data_ptr(), d_out.data_ptr(), d_st.data_ptr(),
+        ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    got = d_out.cpu().numpy().tobytes()            # torch-stream ordered read only
+    ref, rst = native.aggregate_pubkeys_batch(offs, host_pks)
+    assert got == b"".join(ref) and not np.any(rst)
+    # verify_batch_device likewise
+    sks = [3, 5, 7, 11]
+    msg = bytes(range(32))
+    pks = b"".join(O.privtopub(k) for k in sks)
+    sigs = bytearray(native.sign_batch(msg * 4, b"".join(k.to_bytes(32, "big") for k in sks),
+                                       (3).to_bytes(8, "big") * 4))
+    sigs[96 * 2:96 * 3] = sigs[0:96]
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_v = torch.zeros(4, dtype=torch.uint8, device=dev)
+    vws = torch.empty(L.bls381_verify_batch_workspace_size(4), dtype=torch.uint8, device=dev)
+    keep = [t(pks), t(msg * 4), t(bytes(sigs)), t((3).to_bytes(8, "big") * 4)]   # alive across the call
+    native.check(L.bls381_verify_batch_device(4, *[x.data_ptr() for x in keep], d_v.data_ptr(),
+                                              vws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    assert d_v.cpu().tolist() == [1, 1, 0, 1]

@@ -7,7 +7,7 @@ TAG=${1:-r01}
 STEPS=${BENCH_STEPS:-3}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests/ -x -q -m gpu -p no:cacheprovider > gpurun_out/gpu_tests_$TAG.log 2>&1 \
+timeout -k 10 600 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests_$TAG.log 2>&1 \
  && echo "tests ok" \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
  && echo "smoke ok" \
