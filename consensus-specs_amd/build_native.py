@@ -28,7 +28,7 @@ def _newer(target, deps):
 
 
 def _run(cmd):
-    print("+", " ".join(cmd), flush=True)
+    print("+", " ".join(cmd), file=sys.stderr, flush=True)
     subprocess.run(cmd, check=True)
 
 

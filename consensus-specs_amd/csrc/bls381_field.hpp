@@ -127,8 +127,7 @@ BLS_INLINE fp_t fp_half(const fp_t& a) {
 // value(a) * value(b) < 2900 q^2 (e.g. both < 4q lazily summed).  Output:
 // normalized, value < 2q.  Column k accumulates <= 14 products < 2^60 plus
 // <= 14 reduction products < 2^56 and a carry < 2^36: < 2^64.
-BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) {
-  BLS_COUNT_FP_MUL();
+BLS_INLINE fp_t fp_mul_body(const fp_t& a, const fp_t& b) {
   uint64_t T[28];
 #pragma unroll
   for (int k = 0; k < 28; ++k) T[k] = 0;
@@ -155,8 +154,7 @@ BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) {
 }
 
 // squaring: 105 products instead of 196 (cross products doubled via 2a_i)
-BLS_NOINLINE fp_t fp_sqr(fp_t a) {
-  BLS_COUNT_FP_MUL();
+BLS_INLINE fp_t fp_sqr_body(const fp_t& a) {
   uint64_t T[28];
   uint32_t a2[14];
 #pragma unroll
@@ -186,6 +184,32 @@ BLS_NOINLINE fp_t fp_sqr(fp_t a) {
   }
   return r;
 }
+
+// Call boundary.  clang passes an aggregate argument in registers only while the
+// aggregates of a call fit 16 VGPRs, so a second fp_t operand would travel
+// through scratch; 14-lane vectors are passed in v0..v27 and returned in v0..v13.
+#if defined(__clang__)
+typedef uint32_t fpv_t __attribute__((ext_vector_type(14)));
+BLS_INLINE fpv_t fp_pack(const fp_t& a) {
+  fpv_t v;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) v[k] = a.w[k];
+  return v;
+}
+BLS_INLINE fp_t fp_unpack(const fpv_t& v) {
+  fp_t a;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) a.w[k] = v[k];
+  return a;
+}
+BLS_NOINLINE fpv_t fp_mul_call(fpv_t a, fpv_t b) { return fp_pack(fp_mul_body(fp_unpack(a), fp_unpack(b))); }
+BLS_NOINLINE fpv_t fp_sqr_call(fpv_t a) { return fp_pack(fp_sqr_body(fp_unpack(a))); }
+BLS_INLINE fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_unpack(fp_mul_call(fp_pack(a), fp_pack(b))); }
+BLS_INLINE fp_t fp_sqr(const fp_t& a) { return fp_unpack(fp_sqr_call(fp_pack(a))); }
+#else
+BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) { BLS_COUNT_FP_MUL(); return fp_mul_body(a, b); }
+BLS_NOINLINE fp_t fp_sqr(fp_t a) { BLS_COUNT_FP_MUL(); return fp_sqr_body(a); }
+#endif
 
 // k * a for a small constant k (k * 2q < 2^31): limb scale, then reduce mod 2q
 BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
