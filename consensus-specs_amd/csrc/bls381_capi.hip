@@ -200,13 +200,13 @@ VerifyWs carve_verify(void* ws, size_t n) {
 int run_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* doms,
                      uint8_t* verdicts, void* ws, hipStream_t s) {
   VerifyWs w = carve_verify(ws, n);
-  const dim3 g(grid_for(n)), b(KBLOCK);
+  const dim3 g(grid_for(n)), g2(grid_for(2 * n)), b(KBLOCK);   // G1: lane per item; G2/Fp12: lane pair
   LAUNCH("decode_g1", s, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
-  LAUNCH("decode_g2", s, g, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
-  LAUNCH("hash_to_g2", s, g, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
-  LAUNCH("miller_loop_2", s, g, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
+  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
+  LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
          (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
-  LAUNCH("final_exp", s, g, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
+  LAUNCH("final_exp", s, g2, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
   return 0;
 }
 
@@ -365,7 +365,7 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* pks, con
 }
 
 // one Miller loop per pair; statuses: any BAD operand -> BAD, an infinite operand -> 1
-__global__ void __launch_bounds__(KBLOCK) k_miller_pairs_batch(size_t npairs, const int32_t* __restrict__ src,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_pairs_batch(size_t npairs, const int32_t* __restrict__ src,
                                                               size_t G, const uint32_t* __restrict__ h_aff,
                                                               const uint8_t* __restrict__ h_st,
                                                               const uint32_t* __restrict__ agg_aff,
@@ -373,11 +373,11 @@ __global__ void __launch_bounds__(KBLOCK) k_miller_pairs_batch(size_t npairs, co
                                                               const uint32_t* __restrict__ sig_aff,
                                                               const uint8_t* __restrict__ sig_st,
                                                               uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t k = item_index<2>();
   if (k >= npairs) return;
   const int32_t s = src[k];
   uint8_t sq, sp;
-  aff_t<fp2_t> Q;
+  aff_t<fp2p_t> Q;
   aff_t<fp_t> P;
   if (s >= 0) {
     sq = h_st[s];
@@ -389,31 +389,31 @@ __global__ void __launch_bounds__(KBLOCK) k_miller_pairs_batch(size_t npairs, co
     sp = ST_OK;
     if (sq == ST_OK) { Q = soa_ld_g2(sig_aff, ncalls, c); P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M; }
   }
-  fp12_t f = fp12_one();
+  fp12p_t f = fp12_one<fp2p_t>();
   uint8_t st = ST_OK;
   if (sq == ST_BAD || sp == ST_BAD) st = ST_BAD;
   else if (sq == ST_OK && sp == ST_OK) f = miller_loop_1(Q, g1_prepare(P));
   soa_st12(f_out, npairs, k, f);
-  st_out[k] = st;
+  if (!pr_odd()) st_out[k] = st;
 }
 
 // each lane multiplies one chunk [begin, end) of Fp12 values (statuses OR-ed);
 // an empty chunk yields 1 (the empty product of an empty call)
-__global__ void __launch_bounds__(KBLOCK) k_fp12_chunk_product(size_t nchunks, const agg_chunk* __restrict__ chunks,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_chunk_product(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                               const uint32_t* __restrict__ in, size_t n_in,
                                                               const uint8_t* __restrict__ in_st,
                                                               uint32_t* __restrict__ out, uint8_t* __restrict__ out_st) {
-  const size_t c = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t c = item_index<2>();
   if (c >= nchunks) return;
   const agg_chunk ch = chunks[c];
-  fp12_t a = fp12_one();
+  fp12p_t a = fp12_one<fp2p_t>();
   uint8_t st = ST_OK;
   for (uint32_t e = ch.begin; e < ch.end; ++e) {
     a = (e == ch.begin) ? soa_ld12(in, n_in, e) : fp12_mul(a, soa_ld12(in, n_in, e));
     if (in_st[e] != ST_OK) st = ST_BAD;
   }
   soa_st12(out, nchunks, c, a);
-  out_st[c] = st;
+  if (!pr_odd()) out_st[c] = st;
 }
 
 // Runs a planned batch up to (and excluding) the final exponentiation.  Returns
@@ -445,17 +445,17 @@ int run_vm_batch(const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hi
     if (rc) return rc;
     b.off += used;
     LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
-    LAUNCH("hash_to_g2", s, dim3(grid_for(G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
+    LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
            (const uint8_t*)d_doms, 8, h_aff, h_st);
   }
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
-  LAUNCH("decode_g2", s, dim3(grid_for(ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs, sig_aff,
+  LAUNCH("decode_g2", s, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs, sig_aff,
          sig_st, 1);
   uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * (np + 1));
   uint8_t* st = b.take<uint8_t>(np + 1);
   if (np)
-    LAUNCH("miller_loop_1", s, dim3(grid_for(np)), dim3(KBLOCK), k_miller_pairs_batch, np, (const int32_t*)d_src, G,
+    LAUNCH("miller_loop_1", s, dim3(grid_for(2 * np)), dim3(KBLOCK), k_miller_pairs_batch, np, (const int32_t*)d_src, G,
            (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
            (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
   // segmented products (chunk lists live in the plan, which outlives the stream work)
@@ -465,7 +465,7 @@ int run_vm_batch(const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hi
     uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
     uint8_t* nst = b.take<uint8_t>(chunks.size());
     HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
-    LAUNCH("fp12_product", s, dim3(grid_for(chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
+    LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
            (const agg_chunk*)d_ch, (const uint32_t*)f, n_in, (const uint8_t*)st, nf, nst);
     f = nf;
     st = nst;
@@ -642,7 +642,7 @@ int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const
   uint8_t* st;
   if ((rc = run_vm_batch(pl, msg_len, sigs, b, c->stream, &f, &st))) return rc;
   uint8_t* d_v = b.take<uint8_t>(n_calls);
-  LAUNCH("final_exp", c->stream, dim3(grid_for(n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
+  LAUNCH("final_exp", c->stream, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
          (const uint32_t*)f, (const uint8_t*)st, d_v);
   HIPC(hipMemcpyAsync(verdicts, d_v, n_calls, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
@@ -677,8 +677,7 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
   uint8_t* st;
   if ((rc = run_vm_batch(pl, msg_len, sig, b, c->stream, &f, &st))) return rc;
   uint8_t* d_out = b.take<uint8_t>(576);
-  LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(64), k_fp12_to_bytes, (const uint32_t*)f, (size_t)1, (size_t)0,
-         d_out);
+  LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(KBLOCK), k_fp12_to_bytes, (size_t)1, (const uint32_t*)f, d_out);
   uint8_t h_st = 0;
   HIPC(hipMemcpyAsync(out576, d_out, 576, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipMemcpyAsync(&h_st, st, 1, hipMemcpyDeviceToHost, c->stream));
@@ -703,7 +702,7 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) try {
   uint8_t* st = b.take<uint8_t>(k);
   HIPC(hipMemcpyAsync(d_in, parts576, 576 * k, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(st, 0, k, s));
-  LAUNCH("fp12_from_bytes", s, dim3(grid_for(k)), dim3(KBLOCK), k_fp12_from_bytes, k, (const uint8_t*)d_in, f);
+  LAUNCH("fp12_from_bytes", s, dim3(grid_for(2 * k)), dim3(KBLOCK), k_fp12_from_bytes, k, (const uint8_t*)d_in, f);
   const auto passes = plan_products({0u, (uint32_t)k});
   size_t n_in = k;
   for (const auto& chunks : passes) {
@@ -711,7 +710,7 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) try {
     uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
     uint8_t* nst = b.take<uint8_t>(chunks.size());
     HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
-    LAUNCH("fp12_product", s, dim3(grid_for(chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
+    LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
            (const agg_chunk*)d_ch, (const uint32_t*)f, n_in, (const uint8_t*)st, nf, nst);
     f = nf;
     st = nst;
@@ -741,8 +740,8 @@ static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets,
   int rc;
   (void)n_pts;
   if (is_g2) {
-    if ((rc = run_agg<fp2_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
-    LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp2_t>, ng, jac, bad, d_out, d_status);
+    if ((rc = run_agg<fp2p_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
+    LAUNCH("agg_compress", s, dim3(grid_for(2 * ng)), dim3(KBLOCK), k_agg_compress<fp2p_t>, ng, jac, bad, d_out, d_status);
   } else {
     if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
@@ -862,7 +861,7 @@ int bls381_sign_batch(size_t n, const uint8_t* msgs32, const uint8_t* sks, const
   HIPC(hipMemcpyAsync(d_msg, msgs32, 32 * n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_sk, sks, 32 * n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_dom, dom8s, 8 * n, hipMemcpyHostToDevice, s));
-  LAUNCH("sign", s, dim3(grid_for(n)), dim3(KBLOCK), k_sign, n, (const uint8_t*)d_msg, (uint32_t)32,
+  LAUNCH("sign", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_sign, n, (const uint8_t*)d_msg, (uint32_t)32,
          (const uint8_t*)d_sk, (const uint8_t*)d_dom, d_out);
   HIPC(hipMemcpyAsync(out96, d_out, 96 * n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -959,7 +958,7 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
   hipStream_t s = c->stream;
   HIPC(hipMemcpyAsync(d_msgs, msgs32, 32 * n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n, hipMemcpyHostToDevice, s));
-  LAUNCH("hash_to_g2_pyecc", s, dim3(grid_for(n, 64)), dim3(64), k_hash_g2_pyecc, n, (const uint8_t*)d_msgs,
+  LAUNCH("hash_to_g2_pyecc", s, dim3(grid_for(2 * n, 64)), dim3(64), k_hash_g2_pyecc, n, (const uint8_t*)d_msgs,
          (const uint8_t*)d_doms, d_scr, d_out);
   HIPC(hipMemcpyAsync(out288, d_out, 288 * n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));

@@ -264,20 +264,22 @@ BLS_HD inline bool g1_in_subgroup(const aff_t<fp_t>& p) {
 }
 
 // psi(x, y) = (cx * conj(x), cy * conj(y)) on E'(Fp2)
-BLS_INLINE aff_t<fp2_t> g2_psi(const aff_t<fp2_t>& a) {
-  aff_t<fp2_t> r;
-  r.x = fp2_mul(PSI_CX_M, fp2_conj(a.x));
-  r.y = fp2_mul(PSI_CY_M, fp2_conj(a.y));
+template <class E>
+BLS_INLINE aff_t<E> g2_psi(const aff_t<E>& a) {
+  aff_t<E> r;
+  r.x = fp2_mul(e2_k<E>(PSI_CX_M), fp2_conj(a.x));
+  r.y = fp2_mul(e2_k<E>(PSI_CY_M), fp2_conj(a.y));
   return r;
 }
 
 // G2: Q in G2 iff psi(Q) == [x]Q = -[|x|]Q
-BLS_HD inline bool g2_in_subgroup(const aff_t<fp2_t>& q) {
-  const jac_t<fp2_t> t = jac_mul_u64(q, BLS_X_ABS);
+template <class E>
+BLS_HD inline bool g2_in_subgroup(const aff_t<E>& q) {
+  const jac_t<E> t = jac_mul_u64(q, BLS_X_ABS);
   if (jac_is_inf(t)) return false;
-  const aff_t<fp2_t> s = g2_psi(q);
-  const fp2_t zz = fp2_sqr(t.z);
-  const fp2_t zzz = fp2_mul(zz, t.z);
+  const aff_t<E> s = g2_psi(q);
+  const E zz = fp2_sqr(t.z);
+  const E zzz = fp2_mul(zz, t.z);
   return fp2_eq(fp2_mul(s.x, zz), t.x) && fp2_eq(fp2_mul(s.y, zzz), fp2_neg(t.y));
 }
 

@@ -35,10 +35,15 @@ constexpr uint32_t FP_MASK = (1u << 28) - 1;
 struct fp_t { uint32_t w[14]; };
 // Fp2 = Fp[u]/(u^2+1): c0 + c1 u
 struct fp2_t { fp_t c0, c1; };
-// Fp6 = Fp2[v]/(v^3 - (1+u))
-struct fp6_t { fp2_t c0, c1, c2; };
-// Fp12 = Fp6[w]/(w^2 - v): c0 + c1 w
-struct fp12_t { fp6_t c0, c1; };
+// Fp6 = Fp2[v]/(v^3 - (1+u)) and Fp12 = Fp6[w]/(w^2 - v): c0 + c1 w, generic
+// over the Fp2 representation E (fp2_t here; the lane-pair fp2p_t of
+// bls381_pair.hpp in the kernels)
+template <class E> struct fp6_g { E c0, c1, c2; };
+template <class E> struct fp12_g { fp6_g<E> c0, c1; };
+using fp6_t = fp6_g<fp2_t>;
+using fp12_t = fp12_g<fp2_t>;
+// Fp2 held by an adjacent lane pair: lane 2i+p holds coefficient p of item i
+struct fp2p_t { fp_t v; };
 
 // Jacobian points (X/Z^2, Y/Z^3); Z == 0 is the point at infinity
 struct g1_jac { fp_t x, y, z; };

@@ -449,36 +449,52 @@ BLS_HD inline bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   return true;
 }
 
-// ---------------------------------------------------------------- Fp6 -----
-BLS_INLINE fp6_t fp6_zero() { fp6_t r; r.c0 = fp2_zero(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
-BLS_INLINE fp6_t fp6_one() { fp6_t r; r.c0 = fp2_one(); r.c1 = fp2_zero(); r.c2 = fp2_zero(); return r; }
-BLS_INLINE fp6_t fp6_add(const fp6_t& a, const fp6_t& b) { fp6_t r; r.c0 = fp2_add(a.c0, b.c0); r.c1 = fp2_add(a.c1, b.c1); r.c2 = fp2_add(a.c2, b.c2); return r; }
-BLS_INLINE fp6_t fp6_sub(const fp6_t& a, const fp6_t& b) { fp6_t r; r.c0 = fp2_sub(a.c0, b.c0); r.c1 = fp2_sub(a.c1, b.c1); r.c2 = fp2_sub(a.c2, b.c2); return r; }
-BLS_INLINE fp6_t fp6_neg(const fp6_t& a) { fp6_t r; r.c0 = fp2_neg(a.c0); r.c1 = fp2_neg(a.c1); r.c2 = fp2_neg(a.c2); return r; }
-BLS_INLINE bool fp6_is_zero(const fp6_t& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }
+// ------------------------------------------- representation-generic tower --
+// Fp6 / Fp12 and everything above them are templates over the Fp2
+// representation E: fp2_t (both coefficients in one lane; the host unit-test
+// build) or fp2p_t (bls381_pair.hpp: the two coefficients in the two lanes of
+// an adjacent lane pair; the gfx950 kernels).  Both provide the same fp2_*
+// operations, so the formulas below exist once.
+template <class E> BLS_INLINE E e2_zero();
+template <class E> BLS_INLINE E e2_one();
+template <class E> BLS_INLINE E e2_k(const fp2_t& k);   // a compile-time Fp2 constant
+template <> BLS_INLINE fp2_t e2_zero<fp2_t>() { return fp2_zero(); }
+template <> BLS_INLINE fp2_t e2_one<fp2_t>() { return fp2_one(); }
+template <> BLS_INLINE fp2_t e2_k<fp2_t>(const fp2_t& k) { return k; }
 
-BLS_NOINLINE fp6_t fp6_mul(const fp6_t& a, const fp6_t& b) {
-  const fp2_t t0 = fp2_mul(a.c0, b.c0);
-  const fp2_t t1 = fp2_mul(a.c1, b.c1);
-  const fp2_t t2 = fp2_mul(a.c2, b.c2);
-  fp6_t r;
+// ---------------------------------------------------------------- Fp6 -----
+template <class E> BLS_INLINE fp6_g<E> fp6_zero() { fp6_g<E> r; r.c0 = e2_zero<E>(); r.c1 = e2_zero<E>(); r.c2 = e2_zero<E>(); return r; }
+template <class E> BLS_INLINE fp6_g<E> fp6_one() { fp6_g<E> r; r.c0 = e2_one<E>(); r.c1 = e2_zero<E>(); r.c2 = e2_zero<E>(); return r; }
+template <class E> BLS_INLINE fp6_g<E> fp6_add(const fp6_g<E>& a, const fp6_g<E>& b) { fp6_g<E> r; r.c0 = fp2_add(a.c0, b.c0); r.c1 = fp2_add(a.c1, b.c1); r.c2 = fp2_add(a.c2, b.c2); return r; }
+template <class E> BLS_INLINE fp6_g<E> fp6_sub(const fp6_g<E>& a, const fp6_g<E>& b) { fp6_g<E> r; r.c0 = fp2_sub(a.c0, b.c0); r.c1 = fp2_sub(a.c1, b.c1); r.c2 = fp2_sub(a.c2, b.c2); return r; }
+template <class E> BLS_INLINE fp6_g<E> fp6_neg(const fp6_g<E>& a) { fp6_g<E> r; r.c0 = fp2_neg(a.c0); r.c1 = fp2_neg(a.c1); r.c2 = fp2_neg(a.c2); return r; }
+template <class E> BLS_INLINE bool fp6_is_zero(const fp6_g<E>& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }
+
+template <class E>
+BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) {
+  const E t0 = fp2_mul(a.c0, b.c0);
+  const E t1 = fp2_mul(a.c1, b.c1);
+  const E t2 = fp2_mul(a.c2, b.c2);
+  fp6_g<E> r;
   r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b.c1, b.c2)), fp2_add(t1, t2))));
   r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
   r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), fp2_add(t0, t2)), t1);
   return r;
 }
 
-BLS_INLINE fp6_t fp6_mul_by_v(const fp6_t& a) {
-  fp6_t r; r.c0 = fp2_mul_xi(a.c2); r.c1 = a.c0; r.c2 = a.c1; return r;
+template <class E>
+BLS_INLINE fp6_g<E> fp6_mul_by_v(const fp6_g<E>& a) {
+  fp6_g<E> r; r.c0 = fp2_mul_xi(a.c2); r.c1 = a.c0; r.c2 = a.c1; return r;
 }
 
-BLS_HD inline fp6_t fp6_inv(const fp6_t& a) {
-  const fp2_t c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
-  const fp2_t c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
-  const fp2_t c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
-  const fp2_t t = fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2))));
-  const fp2_t ti = fp2_inv(t);
-  fp6_t r;
+template <class E>
+BLS_HD inline fp6_g<E> fp6_inv(const fp6_g<E>& a) {
+  const E c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
+  const E c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
+  const E c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
+  const E t = fp2_add(fp2_mul(a.c0, c0), fp2_mul_xi(fp2_add(fp2_mul(a.c2, c1), fp2_mul(a.c1, c2))));
+  const E ti = fp2_inv(t);
+  fp6_g<E> r;
   r.c0 = fp2_mul(c0, ti);
   r.c1 = fp2_mul(c1, ti);
   r.c2 = fp2_mul(c2, ti);
@@ -486,21 +502,24 @@ BLS_HD inline fp6_t fp6_inv(const fp6_t& a) {
 }
 
 // ---------------------------------------------------------------- Fp12 ----
-BLS_INLINE fp12_t fp12_one() { fp12_t r; r.c0 = fp6_one(); r.c1 = fp6_zero(); return r; }
+template <class E> BLS_INLINE fp12_g<E> fp12_one() { fp12_g<E> r; r.c0 = fp6_one<E>(); r.c1 = fp6_zero<E>(); return r; }
 
-BLS_INLINE bool fp12_is_one(const fp12_t& a) {
-  return fp2_eq(a.c0.c0, fp2_one()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp6_is_zero(a.c1);
+template <class E>
+BLS_INLINE bool fp12_is_one(const fp12_g<E>& a) {
+  return fp2_eq(a.c0.c0, e2_one<E>()) && fp2_is_zero(a.c0.c1) && fp2_is_zero(a.c0.c2) && fp6_is_zero(a.c1);
 }
 
-BLS_INLINE bool fp12_eq(const fp12_t& a, const fp12_t& b) {
+template <class E>
+BLS_INLINE bool fp12_eq(const fp12_g<E>& a, const fp12_g<E>& b) {
   return fp2_eq(a.c0.c0, b.c0.c0) && fp2_eq(a.c0.c1, b.c0.c1) && fp2_eq(a.c0.c2, b.c0.c2) &&
          fp2_eq(a.c1.c0, b.c1.c0) && fp2_eq(a.c1.c1, b.c1.c1) && fp2_eq(a.c1.c2, b.c1.c2);
 }
 
-BLS_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
-  const fp6_t ac = fp6_mul(a.c0, b.c0);
-  const fp6_t bd = fp6_mul(a.c1, b.c1);
-  fp12_t r;
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
+  const fp6_g<E> ac = fp6_mul(a.c0, b.c0);
+  const fp6_g<E> bd = fp6_mul(a.c1, b.c1);
+  fp12_g<E> r;
   r.c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), ac), bd);
   r.c0 = fp6_add(ac, fp6_mul_by_v(bd));
   return r;
@@ -508,35 +527,39 @@ BLS_NOINLINE fp12_t fp12_mul(const fp12_t& a, const fp12_t& b) {
 
 // complex squaring: (a + b w)^2 = (a^2 + v b^2) + 2ab w
 //   = ((a + b)(a + v b) - ab - v ab) + 2ab w
-BLS_NOINLINE fp12_t fp12_sqr(const fp12_t& f) {
-  const fp6_t ab = fp6_mul(f.c0, f.c1);
-  const fp6_t t = fp6_mul(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
-  fp12_t r;
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_sqr(const fp12_g<E>& f) {
+  const fp6_g<E> ab = fp6_mul(f.c0, f.c1);
+  const fp6_g<E> t = fp6_mul(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
+  fp12_g<E> r;
   r.c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_by_v(ab));
   r.c1 = fp6_add(ab, ab);
   return r;
 }
 
-BLS_INLINE fp12_t fp12_conj(const fp12_t& a) { fp12_t r; r.c0 = a.c0; r.c1 = fp6_neg(a.c1); return r; }
+template <class E>
+BLS_INLINE fp12_g<E> fp12_conj(const fp12_g<E>& a) { fp12_g<E> r; r.c0 = a.c0; r.c1 = fp6_neg(a.c1); return r; }
 
-BLS_HD inline fp12_t fp12_inv(const fp12_t& f) {
-  const fp6_t t = fp6_sub(fp6_mul(f.c0, f.c0), fp6_mul_by_v(fp6_mul(f.c1, f.c1)));
-  const fp6_t ti = fp6_inv(t);
-  fp12_t r;
+template <class E>
+BLS_HD inline fp12_g<E> fp12_inv(const fp12_g<E>& f) {
+  const fp6_g<E> t = fp6_sub(fp6_mul(f.c0, f.c0), fp6_mul_by_v(fp6_mul(f.c1, f.c1)));
+  const fp6_g<E> ti = fp6_inv(t);
+  fp12_g<E> r;
   r.c0 = fp6_mul(f.c0, ti);
   r.c1 = fp6_neg(fp6_mul(f.c1, ti));
   return r;
 }
 
 // f^(q^p), p in {1,2,3}; coefficient of w^k picks up gamma[p][k] (and conj for odd p)
-BLS_HD inline fp12_t fp12_frob(const fp12_t& f, int p) {
+template <class E>
+BLS_HD inline fp12_g<E> fp12_frob(const fp12_g<E>& f, int p) {
   const fp2_t* g = FROB_GAMMA_M[p - 1];
   const bool odd = (p & 1) != 0;
-  auto fr = [&](const fp2_t& c, int k) -> fp2_t {
-    const fp2_t cc = odd ? fp2_conj(c) : c;
-    return k == 0 ? cc : fp2_mul(cc, g[k]);
+  auto fr = [&](const E& c, int k) -> E {
+    const E cc = odd ? fp2_conj(c) : c;
+    return k == 0 ? cc : fp2_mul(cc, e2_k<E>(g[k]));
   };
-  fp12_t r;
+  fp12_g<E> r;
   r.c0.c0 = fr(f.c0.c0, 0);
   r.c0.c1 = fr(f.c0.c1, 2);
   r.c0.c2 = fr(f.c0.c2, 4);
@@ -547,35 +570,36 @@ BLS_HD inline fp12_t fp12_frob(const fp12_t& f, int p) {
 }
 
 // sparse product f * (c0 + c1 v + c2 v w): 13 Fp2 multiplications
-BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2_t& c1, const fp2_t& c2) {
-  const fp6_t& a = f.c0;
-  const fp6_t& b = f.c1;
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E& c1, const E& c2) {
+  const fp6_g<E>& a = f.c0;
+  const fp6_g<E>& b = f.c1;
   // aA, A = c0 + c1 v
-  fp6_t aA;
+  fp6_g<E> aA;
   {
-    const fp2_t t0 = fp2_mul(a.c0, c0);
-    const fp2_t t1 = fp2_mul(a.c1, c1);
+    const E t0 = fp2_mul(a.c0, c0);
+    const E t1 = fp2_mul(a.c1, c1);
     aA.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, c1)));
     aA.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(c0, c1)), t0), t1);
     aA.c2 = fp2_add(t1, fp2_mul(a.c2, c0));
   }
   // bB, B = c2 v
-  fp6_t bB;
+  fp6_g<E> bB;
   bB.c0 = fp2_mul_xi(fp2_mul(b.c2, c2));
   bB.c1 = fp2_mul(b.c0, c2);
   bB.c2 = fp2_mul(b.c1, c2);
   // (a + b)(A + B), A + B = c0 + (c1 + c2) v
-  const fp6_t s = fp6_add(a, b);
-  const fp2_t d1 = fp2_add(c1, c2);
-  fp6_t m;
+  const fp6_g<E> s = fp6_add(a, b);
+  const E d1 = fp2_add(c1, c2);
+  fp6_g<E> m;
   {
-    const fp2_t t0 = fp2_mul(s.c0, c0);
-    const fp2_t t1 = fp2_mul(s.c1, d1);
+    const E t0 = fp2_mul(s.c0, c0);
+    const E t1 = fp2_mul(s.c1, d1);
     m.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(s.c2, d1)));
     m.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(s.c0, s.c1), fp2_add_lazy(c0, d1)), t0), t1);
     m.c2 = fp2_add(t1, fp2_mul(s.c2, c0));
   }
-  fp12_t r;
+  fp12_g<E> r;
   r.c0 = fp6_add(aA, fp6_mul_by_v(bB));
   r.c1 = fp6_sub(fp6_sub(m, aA), bB);
   return r;
@@ -585,20 +609,21 @@ BLS_NOINLINE fp12_t fp12_mul_by_line(const fp12_t& f, const fp2_t& c0, const fp2
 // Fp4[w]/(w^3 - z), Fp4 = Fp2[z]/(z^2 - xi), z = w^3:
 //   f = A + B w + C w^2,  A = a0 + b1 z,  B = b0 + a2 z,  C = a1 + b2 z
 //   A' = 3A^2 - 2 conj(A),  B' = 3 z C^2 + 2 conj(B),  C' = 3 B^2 - 2 conj(C)
-BLS_INLINE fp12_t fp12_cyclotomic_sqr_inl(const fp12_t& f) {
-  const fp2_t& a0 = f.c0.c0; const fp2_t& a1 = f.c0.c1; const fp2_t& a2 = f.c0.c2;
-  const fp2_t& b0 = f.c1.c0; const fp2_t& b1 = f.c1.c1; const fp2_t& b2 = f.c1.c2;
-  auto sq4 = [](const fp2_t& x0, const fp2_t& x1, fp2_t& r0, fp2_t& r1) {
-    const fp2_t t0 = fp2_sqr(x0);
-    const fp2_t t1 = fp2_sqr(x1);
+template <class E>
+BLS_INLINE fp12_g<E> fp12_cyclotomic_sqr_inl(const fp12_g<E>& f) {
+  const E& a0 = f.c0.c0; const E& a1 = f.c0.c1; const E& a2 = f.c0.c2;
+  const E& b0 = f.c1.c0; const E& b1 = f.c1.c1; const E& b2 = f.c1.c2;
+  auto sq4 = [](const E& x0, const E& x1, E& r0, E& r1) {
+    const E t0 = fp2_sqr(x0);
+    const E t1 = fp2_sqr(x1);
     r0 = fp2_add(t0, fp2_mul_xi(t1));
     r1 = fp2_sub(fp2_sqr(fp2_add(x0, x1)), fp2_add(t0, t1));
   };
-  fp2_t A0, A1, B0, B1, C0, C1;
+  E A0, A1, B0, B1, C0, C1;
   sq4(a0, b1, A0, A1);
   sq4(b0, a2, B0, B1);
   sq4(a1, b2, C0, C1);
-  fp12_t r;
+  fp12_g<E> r;
   // A'
   r.c0.c0 = fp2_sub(fp2_mul_small(A0, 3), fp2_dbl(a0));
   r.c1.c1 = fp2_add(fp2_mul_small(A1, 3), fp2_dbl(b1));
@@ -611,7 +636,7 @@ BLS_INLINE fp12_t fp12_cyclotomic_sqr_inl(const fp12_t& f) {
   return r;
 }
 
-
-BLS_NOINLINE fp12_t fp12_cyclotomic_sqr(const fp12_t& f) { return fp12_cyclotomic_sqr_inl(f); }
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_cyclotomic_sqr(const fp12_g<E>& f) { return fp12_cyclotomic_sqr_inl(f); }
 
 }  // namespace bls381

@@ -78,7 +78,8 @@ BLS_INLINE fp_t fp_plain_from_digest(const uint32_t d[8]) {
 
 // spec root selection (bls_signature.md:91,107): keep the root whose imaginary
 // part is the larger of {y_im, q - y_im}, ties (y_im == 0) broken on the real part.
-BLS_INLINE fp2_t g2_select_root(const fp2_t& y) {
+template <class E>
+BLS_INLINE E g2_select_root(const E& y) {
   return g2_y_flag(y) ? y : fp2_neg(y);
 }
 
@@ -111,10 +112,11 @@ BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, ui
 }
 
 // psi on Jacobian coordinates: (cx conj(X), cy conj(Y), conj(Z))
-BLS_INLINE jac_t<fp2_t> g2_psi_jac(const jac_t<fp2_t>& p) {
-  jac_t<fp2_t> r;
-  r.x = fp2_mul(PSI_CX_M, fp2_conj(p.x));
-  r.y = fp2_mul(PSI_CY_M, fp2_conj(p.y));
+template <class E>
+BLS_INLINE jac_t<E> g2_psi_jac(const jac_t<E>& p) {
+  jac_t<E> r;
+  r.x = fp2_mul(e2_k<E>(PSI_CX_M), fp2_conj(p.x));
+  r.y = fp2_mul(e2_k<E>(PSI_CY_M), fp2_conj(p.y));
   r.z = fp2_conj(p.z);
   return r;
 }
@@ -129,20 +131,21 @@ BLS_INLINE jac_t<fp2_t> g2_psi_jac(const jac_t<fp2_t>& p) {
 //   Q_i = (-psi)^i BP(P).
 // ~190 doublings + ~45 additions instead of the 508-doubling ladder; the
 // identity is checked in oracle/tower_model.py and tests/test_tower_model.py.
-BLS_HD inline jac_t<fp2_t> g2_mul_cofactor(const aff_t<fp2_t>& p) {
-  aff_t<fp2_t> np;
+template <class E>
+BLS_HD inline jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
+  aff_t<E> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
-  const jac_t<fp2_t> t1 = jac_mul_u64(p, BLS_X_ABS);                  // [|x|]P = -[x]P
-  jac_t<fp2_t> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
+  const jac_t<E> t1 = jac_mul_u64(p, BLS_X_ABS);                  // [|x|]P = -[x]P
+  jac_t<E> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
   Q0 = jac_add(Q0, g2_psi_jac(jac_add_aff(jac_neg(t1), np)));          // + psi([x - 1]P)
   Q0 = jac_add(Q0, g2_psi_jac(g2_psi_jac(jac_dbl(jac_from_aff(p)))));  // + psi^2(2P)
-  const jac_t<fp2_t> Q1 = jac_neg(g2_psi_jac(Q0));
-  const jac_t<fp2_t> Q2 = jac_neg(g2_psi_jac(Q1));
-  const jac_t<fp2_t> T = jac_add(jac_add(jac_dbl(Q2), Q1), jac_neg(g2_psi_jac(Q2)));   // Q1 + 2Q2 + Q3
-  const jac_t<fp2_t> S = jac_add(jac_add(T, Q1), Q0);
-  const jac_t<fp2_t> nS = jac_neg(S);
-  jac_t<fp2_t> R = S;   // leading NAF digit of e0 is +1
+  const jac_t<E> Q1 = jac_neg(g2_psi_jac(Q0));
+  const jac_t<E> Q2 = jac_neg(g2_psi_jac(Q1));
+  const jac_t<E> T = jac_add(jac_add(jac_dbl(Q2), Q1), jac_neg(g2_psi_jac(Q2)));   // Q1 + 2Q2 + Q3
+  const jac_t<E> S = jac_add(jac_add(T, Q1), Q0);
+  const jac_t<E> nS = jac_neg(S);
+  jac_t<E> R = S;   // leading NAF digit of e0 is +1
   for (int i = 1; i < E0_NAF_LEN; ++i) {
     R = jac_dbl(R);
     const int dg = E0_NAF[i];

@@ -1,11 +1,13 @@
-// gfx950 kernels of the BLS12-381 engine.  One work item per lane; every
-// intermediate lives in HBM in structure-of-arrays, limb-major layout
-// (limb k of component c of item i at base[(c*14 + k) * n + i]) so that each
-// limb load/store of a wavefront is one contiguous 256-byte access
-// (DESIGN.md "Data layout in HBM").
+// gfx950 kernels of the BLS12-381 engine.  G1 work runs one item per lane; all
+// G2 / Fp12 work runs one item per adjacent lane pair (bls381_pair.hpp).  Every
+// intermediate lives in HBM in structure-of-arrays, limb-major layout so that
+// each limb load/store of a wavefront is one contiguous 256-byte access
+// (DESIGN.md "Data layout in HBM"):
+//   one-lane items:  limb k of Fp component c of item i at base[(c*14 + k) * n + i]
+//   lane-pair items: limb k of Fp2 component c of item i, coefficient p, at
+//                    base[(c*14 + k) * 2n + 2i + p]   (lane index 2i + p)
 #pragma once
-#include "bls381_hash.hpp"
-#include "bls381_pairing.hpp"
+#include "bls381_pair.hpp"
 
 namespace bls381 {
 
@@ -13,9 +15,10 @@ enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2 };
 
 constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 // minimum waves per SIMD requested from the register allocator for the heavy
-// per-item kernels (1 = up to 512 VGPR+AGPR per lane, 2 = up to 256)
+// per-item kernels (1 = up to 512 VGPR+AGPR per lane, 2 = up to 256).  Two:
+// one wave alone issues a VALU op every 4 cycles, a second fills the other 2.
 #ifndef BLS_WAVES_PER_EU
-#define BLS_WAVES_PER_EU 1
+#define BLS_WAVES_PER_EU 2
 #endif
 
 // ------------------------------------------------------------ SoA access --
@@ -29,33 +32,35 @@ __device__ __forceinline__ void soa_st(uint32_t* __restrict__ p, size_t n, size_
 #pragma unroll
   for (int k = 0; k < FP_LIMBS; ++k) p[(size_t)(c * FP_LIMBS + k) * n + i] = a.w[k];
 }
-__device__ __forceinline__ fp2_t soa_ld2(const uint32_t* p, size_t n, size_t i, int c) {
-  fp2_t r; r.c0 = soa_ld(p, n, i, c); r.c1 = soa_ld(p, n, i, c + 1); return r;
-}
-__device__ __forceinline__ void soa_st2(uint32_t* p, size_t n, size_t i, int c, const fp2_t& a) {
-  soa_st(p, n, i, c, a.c0); soa_st(p, n, i, c + 1, a.c1);
-}
 __device__ __forceinline__ aff_t<fp_t> soa_ld_g1(const uint32_t* p, size_t n, size_t i) {
   aff_t<fp_t> a; a.x = soa_ld(p, n, i, 0); a.y = soa_ld(p, n, i, 1); return a;
 }
 __device__ __forceinline__ void soa_st_g1(uint32_t* p, size_t n, size_t i, const aff_t<fp_t>& a) {
   soa_st(p, n, i, 0, a.x); soa_st(p, n, i, 1, a.y);
 }
-__device__ __forceinline__ aff_t<fp2_t> soa_ld_g2(const uint32_t* p, size_t n, size_t i) {
-  aff_t<fp2_t> a; a.x = soa_ld2(p, n, i, 0); a.y = soa_ld2(p, n, i, 2); return a;
+// lane-pair items: n items, item i, Fp2 component c (this lane's coefficient)
+__device__ __forceinline__ fp2p_t soa_ld2p(const uint32_t* p, size_t n, size_t i, int c) {
+  return pr_make(soa_ld(p, 2 * n, 2 * i + (pr_odd() ? 1 : 0), c));
 }
-__device__ __forceinline__ void soa_st_g2(uint32_t* p, size_t n, size_t i, const aff_t<fp2_t>& a) {
-  soa_st2(p, n, i, 0, a.x); soa_st2(p, n, i, 2, a.y);
+__device__ __forceinline__ void soa_st2p(uint32_t* p, size_t n, size_t i, int c, const fp2p_t& a) {
+  soa_st(p, 2 * n, 2 * i + (pr_odd() ? 1 : 0), c, a.v);
 }
-__device__ __forceinline__ fp12_t soa_ld12(const uint32_t* p, size_t n, size_t i) {
-  fp12_t f;
-  f.c0.c0 = soa_ld2(p, n, i, 0); f.c0.c1 = soa_ld2(p, n, i, 2); f.c0.c2 = soa_ld2(p, n, i, 4);
-  f.c1.c0 = soa_ld2(p, n, i, 6); f.c1.c1 = soa_ld2(p, n, i, 8); f.c1.c2 = soa_ld2(p, n, i, 10);
+__device__ __forceinline__ aff_t<fp2p_t> soa_ld_g2(const uint32_t* p, size_t n, size_t i) {
+  aff_t<fp2p_t> a; a.x = soa_ld2p(p, n, i, 0); a.y = soa_ld2p(p, n, i, 1); return a;
+}
+__device__ __forceinline__ void soa_st_g2(uint32_t* p, size_t n, size_t i, const aff_t<fp2p_t>& a) {
+  soa_st2p(p, n, i, 0, a.x); soa_st2p(p, n, i, 1, a.y);
+}
+using fp12p_t = fp12_g<fp2p_t>;
+__device__ __forceinline__ fp12p_t soa_ld12(const uint32_t* p, size_t n, size_t i) {
+  fp12p_t f;
+  f.c0.c0 = soa_ld2p(p, n, i, 0); f.c0.c1 = soa_ld2p(p, n, i, 1); f.c0.c2 = soa_ld2p(p, n, i, 2);
+  f.c1.c0 = soa_ld2p(p, n, i, 3); f.c1.c1 = soa_ld2p(p, n, i, 4); f.c1.c2 = soa_ld2p(p, n, i, 5);
   return f;
 }
-__device__ __forceinline__ void soa_st12(uint32_t* p, size_t n, size_t i, const fp12_t& f) {
-  soa_st2(p, n, i, 0, f.c0.c0); soa_st2(p, n, i, 2, f.c0.c1); soa_st2(p, n, i, 4, f.c0.c2);
-  soa_st2(p, n, i, 6, f.c1.c0); soa_st2(p, n, i, 8, f.c1.c1); soa_st2(p, n, i, 10, f.c1.c2);
+__device__ __forceinline__ void soa_st12(uint32_t* p, size_t n, size_t i, const fp12p_t& f) {
+  soa_st2p(p, n, i, 0, f.c0.c0); soa_st2p(p, n, i, 1, f.c0.c1); soa_st2p(p, n, i, 2, f.c0.c2);
+  soa_st2p(p, n, i, 3, f.c1.c0); soa_st2p(p, n, i, 4, f.c1.c1); soa_st2p(p, n, i, 5, f.c1.c2);
 }
 template <class F> struct soa_jac;
 template <> struct soa_jac<fp_t> {
@@ -67,13 +72,13 @@ template <> struct soa_jac<fp_t> {
     soa_st(p, n, i, 0, a.x); soa_st(p, n, i, 1, a.y); soa_st(p, n, i, 2, a.z);
   }
 };
-template <> struct soa_jac<fp2_t> {
-  static constexpr int NC = 6;
-  __device__ static jac_t<fp2_t> ld(const uint32_t* p, size_t n, size_t i) {
-    jac_t<fp2_t> r; r.x = soa_ld2(p, n, i, 0); r.y = soa_ld2(p, n, i, 2); r.z = soa_ld2(p, n, i, 4); return r;
+template <> struct soa_jac<fp2p_t> {
+  static constexpr int NC = 6;   // words: 3 Fp2 x 2 lanes
+  __device__ static jac_t<fp2p_t> ld(const uint32_t* p, size_t n, size_t i) {
+    jac_t<fp2p_t> r; r.x = soa_ld2p(p, n, i, 0); r.y = soa_ld2p(p, n, i, 1); r.z = soa_ld2p(p, n, i, 2); return r;
   }
-  __device__ static void st(uint32_t* p, size_t n, size_t i, const jac_t<fp2_t>& a) {
-    soa_st2(p, n, i, 0, a.x); soa_st2(p, n, i, 2, a.y); soa_st2(p, n, i, 4, a.z);
+  __device__ static void st(uint32_t* p, size_t n, size_t i, const jac_t<fp2p_t>& a) {
+    soa_st2p(p, n, i, 0, a.x); soa_st2p(p, n, i, 1, a.y); soa_st2p(p, n, i, 2, a.z);
   }
 };
 
@@ -81,12 +86,23 @@ __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict
   for (int k = 0; k < len; ++k) dst[k] = src[k];
 }
 
+// lanes per item: 1 for G1 (fp_t), 2 for G2 (fp2p_t)
+template <class F> struct lanes_per;
+template <> struct lanes_per<fp_t> { static constexpr int N = 1; };
+template <> struct lanes_per<fp2p_t> { static constexpr int N = 2; };
+
+// grid helper for kernels: item index of this lane (pair kernels: lane / 2)
+template <int LPI>
+__device__ __forceinline__ size_t item_index() {
+  return ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / LPI;
+}
+
 // --------------------------------------------------------- decode kernels --
 // pubkeys -> affine G1 (SoA 2 Fp) + status; optional subgroup check
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      int check_subgroup) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<1>();
   if (i >= n) return;
   uint8_t b[48];
   ld_bytes(b, pks + 48 * i, 48);
@@ -97,40 +113,38 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n
   if (s == PT_OK) soa_st_g1(out, n, i, a);
 }
 
-// signatures -> affine G2 (SoA 4 Fp) + status; optional subgroup check
+// signatures -> affine G2 (pair SoA, 2 Fp2) + status; optional subgroup check
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n, const uint8_t* __restrict__ sigs,
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      int check_subgroup) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
-  uint8_t b[96];
-  ld_bytes(b, sigs + 96 * i, 96);
-  aff_t<fp2_t> a;
-  int s = g2_decompress(a, b);
+  aff_t<fp2p_t> a;
+  int s = g2_decompress(a, sigs + 96 * i);
   if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = PT_BAD;
-  st[i] = (uint8_t)s;
+  if (!pr_odd()) st[i] = (uint8_t)s;
   if (s == PT_OK) soa_st_g2(out, n, i, a);
 }
 
-// (msg, dom8) -> hash_to_G2 affine (SoA 4 Fp).  dom_stride 0 = one shared domain.
+// (msg, dom8) -> hash_to_G2 affine (pair SoA).  dom_stride 0 = one shared domain.
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                    const uint8_t* __restrict__ doms, int dom_stride,
                                                    uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
   uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
-  aff_t<fp2_t> c;
+  aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
-  aff_t<fp2_t> h;
+  aff_t<fp2p_t> h;
   const bool fin = jac_to_aff(h, g2_mul_cofactor(c));
-  if (st) st[i] = fin ? ST_OK : ST_INF;
+  if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
   if (fin) soa_st_g2(out, n, i, h);
 }
 
 // --------------------------------------------------------- verify kernels --
-// One bls_verify per lane: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
+// One bls_verify per lane pair: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
 // infinity short-circuit of py_ecc's pairing (a pair with an infinite point is 1).
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
                                                          const uint8_t* __restrict__ sig_st,
@@ -138,11 +152,12 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size
                                                          const uint8_t* __restrict__ pk_st,
                                                          const uint32_t* __restrict__ h_aff,
                                                          uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
+  const bool lead = !pr_odd();
   const uint8_t ss = sig_st[i], ps = pk_st[i];
-  if (ss == ST_BAD || ps == ST_BAD) { st_out[i] = ST_BAD; return; }
-  aff_t<fp2_t> Q[2];
+  if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
+  aff_t<fp2p_t> Q[2];
   g1_line_pre P[2];
   int np = 0;
   if (ss == ST_OK) {
@@ -156,59 +171,32 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size
     P[np] = g1_prepare(soa_ld_g1(pk_aff, n, i));
     ++np;
   }
-  fp12_t f;
+  fp12p_t f;
   if (np == 2) f = miller_loop_n<2>(Q, P);
   else if (np == 1) f = miller_loop_n<1>(Q, P);
-  else f = fp12_one();
+  else f = fp12_one<fp2p_t>();
   soa_st12(f_out, n, i, f);
-  st_out[i] = ST_OK;
+  if (lead) st_out[i] = ST_OK;
 }
 
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
-  if (st[i] != ST_OK) { verdict[i] = 0; return; }
-  const fp12_t f = soa_ld12(f_in, n, i);
-  verdict[i] = fp12_is_one(final_exp(f)) ? 1 : 0;
-}
-
-// ---------------------------------------------------- multi-pair products --
-// pair k: Q = q_aff[q_idx[k]] (G2 SoA over nq), P = p_aff[p_idx[k]] (G1 SoA over np_)
-// p_idx == -1 selects -g1.  One Miller loop per lane; product tree afterwards.
-__global__ void __launch_bounds__(KBLOCK) k_miller_pairs(size_t npairs, const uint32_t* __restrict__ q_aff, size_t nq,
-                                                        const int32_t* __restrict__ q_idx,
-                                                        const uint32_t* __restrict__ p_aff, size_t np_,
-                                                        const int32_t* __restrict__ p_idx,
-                                                        uint32_t* __restrict__ f_out) {
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= npairs) return;
-  const aff_t<fp2_t> Q = soa_ld_g2(q_aff, nq, (size_t)q_idx[k]);
-  aff_t<fp_t> p;
-  const int32_t pi = p_idx[k];
-  if (pi < 0) { p.x = G1_GEN_X_M; p.y = G1_GEN_NEGY_M; }
-  else p = soa_ld_g1(p_aff, np_, (size_t)pi);
-  const g1_line_pre P = g1_prepare(p);
-  soa_st12(f_out, npairs, k, miller_loop_1(Q, P));
-}
-
-// out[j] = in[2j] * in[2j+1] (in[2j] alone if 2j+1 == m)
-__global__ void __launch_bounds__(KBLOCK) k_fp12_pair_product(size_t m, const uint32_t* __restrict__ in,
-                                                             uint32_t* __restrict__ out) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t half = (m + 1) / 2;
-  if (j >= half) return;
-  fp12_t a = soa_ld12(in, m, 2 * j);
-  if (2 * j + 1 < m) a = fp12_mul(a, soa_ld12(in, m, 2 * j + 1));
-  soa_st12(out, half, j, a);
+  const bool lead = !pr_odd();
+  if (st[i] != ST_OK) { if (lead) verdict[i] = 0; return; }
+  const fp12p_t f = soa_ld12(f_in, n, i);
+  const bool one = fp12_is_one(final_exp(f));
+  if (lead) verdict[i] = one ? 1 : 0;
 }
 
 // ---------------------------------------------------- aggregation kernels --
 // A chunk is a contiguous range [begin, end) of inputs belonging to one group.
-// Each workgroup sums one chunk: lanes stride over the chunk, then a tree
-// reduction of Jacobian partials staged in LDS.  The input is either
-// compressed points (level 1: decode + sum) or Jacobian SoA partials.
+// Each workgroup sums one chunk: item slots (one lane, or one lane pair for G2)
+// stride over the chunk, then a tree reduction of Jacobian partials staged in
+// LDS.  The input is either compressed points (level 1: decode + sum) or
+// Jacobian SoA partials.
 struct agg_chunk { uint32_t begin, end; };
 
 template <class F> struct pt_traits;
@@ -216,18 +204,19 @@ template <> struct pt_traits<fp_t> {
   static constexpr int BYTES = 48;
   __device__ static int decode(aff_t<fp_t>& a, const uint8_t* b) { return g1_decompress(a, b); }
 };
-template <> struct pt_traits<fp2_t> {
+template <> struct pt_traits<fp2p_t> {
   static constexpr int BYTES = 96;
-  __device__ static int decode(aff_t<fp2_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
+  __device__ static int decode(aff_t<fp2p_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
 };
 
 template <class F, bool LEVEL1>
-__global__ void __launch_bounds__(KBLOCK) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                       const uint8_t* __restrict__ in_bytes,
                                                       const uint32_t* __restrict__ in_jac, size_t n_in,
                                                       const uint8_t* __restrict__ in_bad,
                                                       uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad) {
-  constexpr int NW = sizeof(jac_t<F>) / 4;
+  constexpr int LPI = lanes_per<F>::N;
+  constexpr int NW = sizeof(jac_t<F>) / 4;   // words per lane
   __shared__ uint32_t lds[KBLOCK * NW];
   __shared__ int bad_any;
   const size_t c = blockIdx.x;
@@ -237,12 +226,11 @@ __global__ void __launch_bounds__(KBLOCK) k_agg_chunks(size_t nchunks, const agg
   __syncthreads();
   jac_t<F> acc = jac_infinity<F>();
   bool bad = false;
-  for (uint32_t e = ch.begin + threadIdx.x; e < ch.end; e += blockDim.x) {
+  const uint32_t slot = threadIdx.x / LPI;
+  for (uint32_t e = ch.begin + slot; e < ch.end; e += KBLOCK / LPI) {
     if (LEVEL1) {
-      uint8_t b[pt_traits<F>::BYTES];
-      ld_bytes(b, in_bytes + (size_t)pt_traits<F>::BYTES * e, pt_traits<F>::BYTES);
       aff_t<F> a;
-      const int s = pt_traits<F>::decode(a, b);
+      const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
       if (s == PT_BAD) bad = true;
       else if (s == PT_OK) acc = jac_add_aff(acc, a);
     } else {
@@ -251,9 +239,10 @@ __global__ void __launch_bounds__(KBLOCK) k_agg_chunks(size_t nchunks, const agg
     }
   }
   if (bad) bad_any = 1;
-  // tree reduction through LDS (lane-major words: conflict-free stride-1 access)
+  // tree reduction through LDS (lane-major words: conflict-free stride-1 access);
+  // s counts lanes and stays a multiple of LPI, so item slots move whole
   uint32_t* mine = lds;
-  for (int s = KBLOCK / 2; s > 0; s >>= 1) {
+  for (int s = KBLOCK / 2; s >= LPI; s >>= 1) {
     __syncthreads();
     if (threadIdx.x >= s && threadIdx.x < 2 * s) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(&acc);
@@ -268,33 +257,35 @@ __global__ void __launch_bounds__(KBLOCK) k_agg_chunks(size_t nchunks, const agg
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < LPI) {
     soa_jac<F>::st(out_jac, nchunks, c, acc);
-    out_bad[c] = (uint8_t)bad_any;
+    if (threadIdx.x == 0) out_bad[c] = (uint8_t)bad_any;
   }
 }
 
+__device__ __forceinline__ void pt_compress(uint8_t* out, const jac_t<fp_t>& p) { g1_compress(out, p); }
+__device__ __forceinline__ void pt_compress(uint8_t* out, const jac_t<fp2p_t>& p) { g2_compress(out, p); }
+
 // per group: Jacobian sum -> compressed bytes + status
 template <class F>
-__global__ void __launch_bounds__(KBLOCK) k_agg_compress(size_t ng, const uint32_t* __restrict__ jac,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_compress(size_t ng, const uint32_t* __restrict__ jac,
                                                         const uint8_t* __restrict__ bad,
                                                         uint8_t* __restrict__ out, int32_t* __restrict__ status) {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int LPI = lanes_per<F>::N;
+  const size_t g = item_index<LPI>();
   if (g >= ng) return;
-  if (bad[g]) { status[g] = BLS381_EINVAL_POINT; return; }
+  const bool lead = (threadIdx.x % LPI) == 0;
+  if (bad[g]) { if (lead) status[g] = BLS381_EINVAL_POINT; return; }
   const jac_t<F> p = soa_jac<F>::ld(jac, ng, g);
-  uint8_t b[pt_traits<F>::BYTES];
-  if constexpr (pt_traits<F>::BYTES == 48) g1_compress(b, p);
-  else g2_compress(b, p);
-  for (int k = 0; k < pt_traits<F>::BYTES; ++k) out[(size_t)pt_traits<F>::BYTES * g + k] = b[k];
-  status[g] = 0;
+  pt_compress(out + (size_t)pt_traits<F>::BYTES * g, p);
+  if (lead) status[g] = 0;
 }
 
 // per group: Jacobian G1 sum -> affine + status (OK / INF / BAD incl. subgroup)
-__global__ void __launch_bounds__(KBLOCK) k_agg_g1_affine(size_t ng, const uint32_t* __restrict__ jac,
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g1_affine(size_t ng, const uint32_t* __restrict__ jac,
                                                          const uint8_t* __restrict__ bad,
                                                          uint32_t* __restrict__ out_aff, uint8_t* __restrict__ st) {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t g = item_index<1>();
   if (g >= ng) return;
   if (bad[g]) { st[g] = ST_BAD; return; }
   aff_t<fp_t> a;
@@ -312,30 +303,29 @@ __device__ __forceinline__ void scalar_limbs_from_be32(uint32_t k[8], const uint
   }
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_sign(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+// sign = [sk] hash_to_G2(m, d), compressed; one lane pair per item
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_sign(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                 const uint8_t* __restrict__ sks, const uint8_t* __restrict__ doms,
                                                 uint8_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
   uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
-  aff_t<fp2_t> c;
+  aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
-  aff_t<fp2_t> h;
-  uint8_t sig[96];
+  aff_t<fp2p_t> h;
   if (!jac_to_aff(h, g2_mul_cofactor(c))) {
-    g2_compress(sig, jac_infinity<fp2_t>());
+    g2_compress(out + 96 * i, jac_infinity<fp2p_t>());
   } else {
     uint32_t k[8];
     scalar_limbs_from_be32(k, sks + 32 * i);
-    g2_compress(sig, jac_mul_limbs(h, k, 256));
+    g2_compress(out + 96 * i, jac_mul_limbs(h, k, 256));
   }
-  for (int b = 0; b < 96; ++b) out[96 * i + b] = sig[b];
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_privtopub(size_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_privtopub(size_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
+  const size_t i = item_index<1>();
   if (i >= n) return;
   uint32_t k[8];
   scalar_limbs_from_be32(k, sks + 32 * i);
@@ -345,131 +335,128 @@ __global__ void __launch_bounds__(KBLOCK) k_privtopub(size_t n, const uint8_t* _
   for (int b = 0; b < 48; ++b) out[48 * i + b] = pk[b];
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_hash_g2_out(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+// hash_to_G2 -> compressed (96 B) + affine (192 B: x_re, x_im, y_re, y_im) per item
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_out(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                        const uint8_t* __restrict__ doms,
                                                        uint8_t* __restrict__ comp, uint8_t* __restrict__ affb) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
+  const int p = pr_odd() ? 1 : 0;
   uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
-  aff_t<fp2_t> c;
+  aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
-  aff_t<fp2_t> h;
-  uint8_t buf[96];
+  aff_t<fp2p_t> h;
   if (!jac_to_aff(h, g2_mul_cofactor(c))) {
-    g2_compress(buf, jac_infinity<fp2_t>());
-    for (int b = 0; b < 96; ++b) comp[96 * i + b] = buf[b];
-    for (int b = 0; b < 192; ++b) affb[192 * i + b] = 0;
+    g2_compress(comp + 96 * i, jac_infinity<fp2p_t>());
+    for (int b = 0; b < 96; ++b) affb[192 * i + 96 * p + b] = 0;
     return;
   }
-  g2_compress_aff(buf, h);
-  for (int b = 0; b < 96; ++b) comp[96 * i + b] = buf[b];
-  fp_plain_to_be48(affb + 192 * i, fp_from_mont(h.x.c0));
-  fp_plain_to_be48(affb + 192 * i + 48, fp_from_mont(h.x.c1));
-  fp_plain_to_be48(affb + 192 * i + 96, fp_from_mont(h.y.c0));
-  fp_plain_to_be48(affb + 192 * i + 144, fp_from_mont(h.y.c1));
+  g2_compress_aff(comp + 96 * i, h);
+  fp_plain_to_be48(affb + 192 * i + 48 * p, fp_from_mont(h.x.v));
+  fp_plain_to_be48(affb + 192 * i + 96 + 48 * p, fp_from_mont(h.y.v));
 }
 
 // ------------------------------------- py_ecc-exact projective hash_to_G2 --
 // Mirrors py_ecc optimized_bls12_381 homogeneous `double`/`add` and the
 // recursive `multiply` so the un-normalised triple
 // printed by test_generators/bls/main.py:66-72 is reproduced bit for bit.
-struct proj2 { fp2_t x, y, z; };
+template <class E> struct proj2 { E x, y, z; };
 
-__device__ inline proj2 pyecc_double(const proj2& p) {
-  const fp2_t W = fp2_mul_small(fp2_sqr(p.x), 3);
-  const fp2_t S = fp2_mul(p.y, p.z);
-  const fp2_t B = fp2_mul(fp2_mul(p.x, p.y), S);
-  const fp2_t H = fp2_sub(fp2_sqr(W), fp2_mul_small(B, 8));
-  const fp2_t S2 = fp2_sqr(S);
-  proj2 r;
+template <class E>
+__device__ inline proj2<E> pyecc_double(const proj2<E>& p) {
+  const E W = fp2_mul_small(fp2_sqr(p.x), 3);
+  const E S = fp2_mul(p.y, p.z);
+  const E B = fp2_mul(fp2_mul(p.x, p.y), S);
+  const E H = fp2_sub(fp2_sqr(W), fp2_mul_small(B, 8));
+  const E S2 = fp2_sqr(S);
+  proj2<E> r;
   r.x = fp2_mul_small(fp2_mul(H, S), 2);
   r.y = fp2_sub(fp2_mul(W, fp2_sub(fp2_mul_small(B, 4), H)), fp2_mul_small(fp2_mul(fp2_sqr(p.y), S2), 8));
   r.z = fp2_mul_small(fp2_mul(S, S2), 8);
   return r;
 }
 
-__device__ inline proj2 pyecc_add(const proj2& p1, const proj2& p2) {
+template <class E>
+__device__ inline proj2<E> pyecc_add(const proj2<E>& p1, const proj2<E>& p2) {
   if (fp2_is_zero(p1.z) || fp2_is_zero(p2.z)) return fp2_is_zero(p2.z) ? p1 : p2;
-  const fp2_t U1 = fp2_mul(p2.y, p1.z);
-  const fp2_t U2 = fp2_mul(p1.y, p2.z);
-  const fp2_t V1 = fp2_mul(p2.x, p1.z);
-  const fp2_t V2 = fp2_mul(p1.x, p2.z);
+  const E U1 = fp2_mul(p2.y, p1.z);
+  const E U2 = fp2_mul(p1.y, p2.z);
+  const E V1 = fp2_mul(p2.x, p1.z);
+  const E V2 = fp2_mul(p1.x, p2.z);
   if (fp2_eq(V1, V2) && fp2_eq(U1, U2)) return pyecc_double(p1);
-  if (fp2_eq(V1, V2)) { proj2 r; r.x = fp2_one(); r.y = fp2_one(); r.z = fp2_zero(); return r; }
-  const fp2_t U = fp2_sub(U1, U2);
-  const fp2_t V = fp2_sub(V1, V2);
-  const fp2_t V_sq = fp2_sqr(V);
-  const fp2_t V_sq_V2 = fp2_mul(V_sq, V2);
-  const fp2_t V_cu = fp2_mul(V, V_sq);
-  const fp2_t W = fp2_mul(p1.z, p2.z);
-  const fp2_t A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(U), W), V_cu), fp2_mul_small(V_sq_V2, 2));
-  proj2 r;
+  if (fp2_eq(V1, V2)) { proj2<E> r; r.x = e2_one<E>(); r.y = e2_one<E>(); r.z = e2_zero<E>(); return r; }
+  const E U = fp2_sub(U1, U2);
+  const E V = fp2_sub(V1, V2);
+  const E V_sq = fp2_sqr(V);
+  const E V_sq_V2 = fp2_mul(V_sq, V2);
+  const E V_cu = fp2_mul(V, V_sq);
+  const E W = fp2_mul(p1.z, p2.z);
+  const E A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(U), W), V_cu), fp2_mul_small(V_sq_V2, 2));
+  proj2<E> r;
   r.x = fp2_mul(V, A);
   r.y = fp2_sub(fp2_mul(U, fp2_sub(V_sq_V2, A)), fp2_mul(V_cu, U2));
   r.z = fp2_mul(V_cu, W);
   return r;
 }
 
-// scratch: per item H2_BITS proj2 slots (SoA over n * H2_BITS entries, 6 Fp each)
-__global__ void __launch_bounds__(64) k_hash_g2_pyecc(size_t n, const uint8_t* __restrict__ msgs,
+// scratch: per item H2_BITS proj2 slots (pair SoA over n * H2_BITS items, 3 Fp2 each)
+__global__ void __launch_bounds__(64, BLS_WAVES_PER_EU) k_hash_g2_pyecc(size_t n, const uint8_t* __restrict__ msgs,
                                                      const uint8_t* __restrict__ doms,
                                                      uint32_t* __restrict__ scratch, uint8_t* __restrict__ out288) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t i = item_index<2>();
   if (i >= n) return;
+  const int p = pr_odd() ? 1 : 0;
   uint8_t sc[41];
   uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
-  aff_t<fp2_t> c;
+  aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + 32 * i, 32, dom, sc);
   const size_t ns = n * (size_t)H2_BITS;
   auto slot = [&](int b) { return i * (size_t)H2_BITS + b; };
-  proj2 cur;
-  cur.x = c.x; cur.y = c.y; cur.z = fp2_one();
+  proj2<fp2p_t> cur;
+  cur.x = c.x; cur.y = c.y; cur.z = e2_one<fp2p_t>();
   // doublings P_b = double^b(P) for b < top, stored; P_top is the accumulator start
   for (int b = 0; b < H2_BITS - 1; ++b) {
     const size_t s = slot(b);
-    soa_st2(scratch, ns, s, 0, cur.x); soa_st2(scratch, ns, s, 2, cur.y); soa_st2(scratch, ns, s, 4, cur.z);
+    soa_st2p(scratch, ns, s, 0, cur.x); soa_st2p(scratch, ns, s, 1, cur.y); soa_st2p(scratch, ns, s, 2, cur.z);
     cur = pyecc_double(cur);
   }
-  proj2 acc = cur;
+  proj2<fp2p_t> acc = cur;
   for (int b = H2_BITS - 2; b >= 0; --b) {
     if ((H2_LIMBS[b >> 5] >> (b & 31)) & 1u) {
       const size_t s = slot(b);
-      proj2 pb;
-      pb.x = soa_ld2(scratch, ns, s, 0); pb.y = soa_ld2(scratch, ns, s, 2); pb.z = soa_ld2(scratch, ns, s, 4);
+      proj2<fp2p_t> pb;
+      pb.x = soa_ld2p(scratch, ns, s, 0); pb.y = soa_ld2p(scratch, ns, s, 1); pb.z = soa_ld2p(scratch, ns, s, 2);
       acc = pyecc_add(acc, pb);
     }
   }
   uint8_t* o = out288 + 288 * i;
-  const fp2_t* cs[3] = {&acc.x, &acc.y, &acc.z};
-  for (int k = 0; k < 3; ++k) {
-    fp_plain_to_be48(o + 96 * k, fp_from_mont(cs[k]->c0));
-    fp_plain_to_be48(o + 96 * k + 48, fp_from_mont(cs[k]->c1));
-  }
+  fp_plain_to_be48(o + 48 * p, fp_from_mont(acc.x.v));
+  fp_plain_to_be48(o + 96 + 48 * p, fp_from_mont(acc.y.v));
+  fp_plain_to_be48(o + 192 + 48 * p, fp_from_mont(acc.z.v));
 }
 
 // -------------------------------------------------------- Fp12 byte codec --
-__global__ void k_fp12_to_bytes(const uint32_t* __restrict__ f, size_t n, size_t i, uint8_t* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const fp12_t a = soa_ld12(f, n, i);
-  const fp2_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
-  for (int k = 0; k < 6; ++k) {
-    fp_plain_to_be48(out + 96 * k, fp_from_mont(cs[k]->c0));
-    fp_plain_to_be48(out + 96 * k + 48, fp_from_mont(cs[k]->c1));
-  }
+// 576 B per item = a0, a1, a2, b0, b1, b2, each Fp2 as re || im (48 B each)
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_to_bytes(size_t n, const uint32_t* __restrict__ f,
+                                                         uint8_t* __restrict__ out) {
+  const size_t i = item_index<2>();
+  if (i >= n) return;
+  const int p = pr_odd() ? 1 : 0;
+  const fp12p_t a = soa_ld12(f, n, i);
+  const fp2p_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int k = 0; k < 6; ++k) fp_plain_to_be48(out + 576 * i + 96 * k + 48 * p, fp_from_mont(cs[k]->v));
 }
 
-__global__ void __launch_bounds__(KBLOCK) k_fp12_from_bytes(size_t n, const uint8_t* __restrict__ in, uint32_t* __restrict__ f) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_from_bytes(size_t n, const uint8_t* __restrict__ in, uint32_t* __restrict__ f) {
+  const size_t i = item_index<2>();
   if (i >= n) return;
-  fp12_t a;
-  fp2_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
-  for (int k = 0; k < 6; ++k) {
-    cs[k]->c0 = fp_to_mont(fp_plain_from_be48(in + 576 * i + 96 * k));
-    cs[k]->c1 = fp_to_mont(fp_plain_from_be48(in + 576 * i + 96 * k + 48));
-  }
+  const int p = pr_odd() ? 1 : 0;
+  fp12p_t a;
+  fp2p_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int k = 0; k < 6; ++k) cs[k]->v = fp_to_mont(fp_plain_from_be48(in + 576 * i + 96 * k + 48 * p));
   soa_st12(f, n, i, a);
 }
 

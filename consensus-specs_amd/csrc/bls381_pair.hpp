@@ -1,0 +1,304 @@
+// Fp2 on an adjacent lane pair -- the representation the gfx950 kernels use.
+//
+// Lane 2i+p of a wavefront holds coefficient p of item i's Fp2 values (p = 0:
+// real part c0, p = 1: imaginary part c1).  Every Fp2 operation is one Fp
+// operation per lane plus DPP exchanges inside the pair (v_mov_b32_dpp
+// quad_perm, full-rate VALU, no LDS), so:
+//   * an item's Fp12 is 6 Fp per lane (84 VGPRs) instead of 12 (168), which is
+//     what lets the Miller-loop and final-exponentiation kernels run two waves
+//     per SIMD without spilling;
+//   * a batch of n items launches 2n lanes: C2's 2^16 verifications fill 2048
+//     waves, two per SIMD of the 1024 on an MI355X, instead of one;
+//   * Fp2 products fold the subtraction of a0 b0 - a1 b1 into one Montgomery
+//     reduction per lane (lane 0: a0 b0 + a1 (8q - b1); lane 1: a1 b0 + a0 b1).
+// The tower, curve, hash and pairing formulas above this file are templates
+// over the Fp2 representation and are shared with the one-lane fp2_t that the
+// host unit-test build checks against the oracle.
+//
+// Control flow must stay uniform within a pair (both lanes take every branch
+// together; DPP reads the partner's registers): every predicate on an Fp2 value
+// is combined across the pair before it is returned.
+#pragma once
+#include "bls381_hash.hpp"
+#include "bls381_pairing.hpp"
+
+namespace bls381 {
+
+// ------------------------------------------------------------ pair plumbing --
+__device__ __forceinline__ bool pr_odd() { return (threadIdx.x & 1u) != 0; }
+
+// DPP quad_perm controls: lane selects within each group of four lanes
+enum : int {
+  DPP_SWAP = 0xB1,   // [1,0,3,2]: the partner's value
+  DPP_EVEN = 0xA0,   // [0,0,2,2]: the even lane's value (coefficient c0)
+  DPP_ODD = 0xF5,    // [1,1,3,3]: the odd lane's value (coefficient c1)
+};
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t pr_dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ fp_t pr_dpp(const fp_t& a) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = pr_dpp<CTRL>(a.w[k]);
+  return r;
+}
+// a predicate true on both lanes of the pair
+__device__ __forceinline__ bool pr_both(bool b) { return (pr_dpp<DPP_SWAP>((uint32_t)b) & (uint32_t)b) != 0; }
+
+__device__ __forceinline__ fp_t fp_sel(bool c, const fp_t& a, const fp_t& b) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = c ? a.w[k] : b.w[k];
+  return r;
+}
+
+// a + b (add) or a - b (!add) with the choice made per lane; inputs < 2q
+// normalized, output < 2q normalized.  One pass for both lanes of a pair whose
+// lanes need different signs (Fp2 multiplication by xi).
+__device__ __forceinline__ fp_t fp_addsub(const fp_t& a, const fp_t& b, bool add) {
+  const uint32_t m = add ? 0u : ~0u;   // b ^ m + s1 = +-b
+  const uint32_t s1 = add ? 0u : 1u;
+  int32_t d[14], e[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    d[i] = (int32_t)(a.w[i] + (b.w[i] ^ m) + s1);
+    e[i] = d[i] + (int32_t)((Q2_LIMBS[i] ^ ~m) + (1u - s1));   // add: d - 2q, sub: d + 2q
+  }
+  fp_carry(d);
+  fp_carry(e);
+  const bool pick_e = add ? (e[13] >= 0) : (d[13] < 0);
+  fp_t r;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(pick_e ? e[i] : d[i]);
+  return r;
+}
+
+// r = base^e with a per-lane exponent: even lanes use ea, odd lanes eb (nbits
+// covers both).  The multiply runs when either lane of the pair needs it.
+__device__ inline fp_t fp_pow_pair(const fp_t& base, const uint32_t* ea, const uint32_t* eb, int nbits) {
+  const bool odd = pr_odd();
+  fp_t r = FP_ONE_M;
+  for (int i = nbits - 1; i >= 0; --i) {
+    r = fp_sqr(r);
+    const uint32_t w = odd ? eb[i >> 5] : ea[i >> 5];
+    if ((w >> (i & 31)) & 1u) r = fp_mul(r, base);
+  }
+  return r;
+}
+
+// ------------------------------------------------------ Fp2 multiplication --
+// lane 0: a0 b0 + a1 (8q - b1) = Re(ab);  lane 1: a1 b0 + a0 b1 = Im(ab).
+// Operands may be lazy sums (limbs < 2^29, values < 4q).  Column k holds <= 14
+// products < 2^58 plus <= 14 products < 2^59 and the reduction's 14 products
+// < 2^56: < 2^63.5.  The sum is < 48 q^2 < q R, so the result is < 2q.
+__device__ __forceinline__ fp_t fp2p_mul_body(const fp_t& a, const fp_t& b) {
+  const bool odd = pr_odd();
+  const fp_t ao = pr_dpp<DPP_SWAP>(a);
+  const fp_t b0 = pr_dpp<DPP_EVEN>(b);
+  const fp_t b1 = pr_dpp<DPP_ODD>(b);
+  uint32_t w[14];
+#pragma unroll
+  for (int k = 0; k < 14; ++k) w[k] = odd ? b1.w[k] : Q8S_LIMBS[k] - b1.w[k];
+  uint64_t T[28];
+#pragma unroll
+  for (int k = 0; k < 28; ++k) T[k] = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      T[i + j] += (uint64_t)a.w[i] * b0.w[j];
+      T[i + j] += (uint64_t)ao.w[i] * w[j];
+    }
+  return fp_redc_wide(T);
+}
+
+// lane 0: (a0 + a1)(a0 + 8q - a1) = a0^2 - a1^2;  lane 1: (a0 + a0) a1 = 2 a0 a1.
+// Operand normalized (< 2q); the factors stay within fp_mul_body's bounds
+// (limbs < 2^29 and < 2^30.4, values < 4q and < 10q).
+__device__ __forceinline__ fp_t fp2p_sqr_body(const fp_t& a) {
+  const bool odd = pr_odd();
+  const fp_t ao = pr_dpp<DPP_SWAP>(a);
+  fp_t x, y;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    x.w[k] = ao.w[k] + (odd ? ao.w[k] : a.w[k]);
+    y.w[k] = odd ? a.w[k] : a.w[k] + Q8S_LIMBS[k] - ao.w[k];
+  }
+  return fp_mul_body(x, y);
+}
+
+__device__ __attribute__((noinline)) fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
+  return fp_pack(fp2p_mul_body(fp_unpack(a), fp_unpack(b)));
+}
+__device__ __attribute__((noinline)) fpv_t fp2p_sqr_call(fpv_t a) { return fp_pack(fp2p_sqr_body(fp_unpack(a))); }
+
+// ------------------------------------------------------------ Fp2 on a pair --
+__device__ __forceinline__ fp2p_t pr_make(const fp_t& v) { fp2p_t r; r.v = v; return r; }
+
+template <> BLS_INLINE fp2p_t e2_zero<fp2p_t>() { return pr_make(fp_zero()); }
+template <> BLS_INLINE fp2p_t e2_one<fp2p_t>() { return pr_make(fp_sel(pr_odd(), fp_zero(), FP_ONE_M)); }
+template <> BLS_INLINE fp2p_t e2_k<fp2p_t>(const fp2_t& k) { return pr_make(fp_sel(pr_odd(), k.c1, k.c0)); }
+
+__device__ __forceinline__ fp2p_t fp2_add(const fp2p_t& a, const fp2p_t& b) { return pr_make(fp_add(a.v, b.v)); }
+__device__ __forceinline__ fp2p_t fp2_sub(const fp2p_t& a, const fp2p_t& b) { return pr_make(fp_sub(a.v, b.v)); }
+__device__ __forceinline__ fp2p_t fp2_neg(const fp2p_t& a) { return pr_make(fp_neg(a.v)); }
+__device__ __forceinline__ fp2p_t fp2_dbl(const fp2p_t& a) { return pr_make(fp_dbl(a.v)); }
+__device__ __forceinline__ fp2p_t fp2_half(const fp2p_t& a) { return pr_make(fp_half(a.v)); }
+__device__ __forceinline__ fp2p_t fp2_add_lazy(const fp2p_t& a, const fp2p_t& b) { return pr_make(fp_add_lazy(a.v, b.v)); }
+__device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) { return pr_make(fp_mul(a.v, s)); }
+__device__ __forceinline__ fp2p_t fp2_mul_small(const fp2p_t& a, int k) { return pr_make(fp_mul_small(a.v, k)); }
+__device__ __forceinline__ fp2p_t fp2_conj(const fp2p_t& a) { return pr_make(fp_sel(pr_odd(), fp_neg(a.v), a.v)); }
+// xi = 1 + u:  (a0 - a1) + (a0 + a1) u
+__device__ __forceinline__ fp2p_t fp2_mul_xi(const fp2p_t& a) {
+  return pr_make(fp_addsub(a.v, pr_dpp<DPP_SWAP>(a.v), pr_odd()));
+}
+__device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
+  return pr_make(fp_unpack(fp2p_mul_call(fp_pack(a.v), fp_pack(b.v))));
+}
+__device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) { return pr_make(fp_unpack(fp2p_sqr_call(fp_pack(a.v)))); }
+__device__ __forceinline__ bool fp2_is_zero(const fp2p_t& a) { return pr_both(fp_is_zero(a.v)); }
+__device__ __forceinline__ bool fp2_eq(const fp2p_t& a, const fp2p_t& b) { return pr_both(fp_eq(a.v, b.v)); }
+
+// 1/a = conj(a) / (a0^2 + a1^2); the norm and its inverse are computed on both lanes
+__device__ inline fp2p_t fp2_inv(const fp2p_t& a) {
+  const fp_t t = fp_sqr(a.v);
+  const fp_t ni = fp_inv(fp_add(t, pr_dpp<DPP_SWAP>(t)));
+  const fp_t r = fp_mul(a.v, ni);
+  return pr_make(fp_sel(pr_odd(), fp_neg(r), r));
+}
+
+// Complex-method square root (same root set as the one-lane fp2_sqrt, so the
+// spec's selection rule picks the same root).  With gamma = sqrt(a0^2 + a1^2)
+// and delta = (a0 + gamma)/2, the even lane raises delta to (q+1)/4 (= t) while
+// the odd lane raises it to (3q-5)/4 (= 1/t) in the same loop; the root is
+// (t, a1/(2t)) when t^2 = delta and (a1/(2t), t) otherwise.
+__device__ inline bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
+  const bool odd = pr_odd();
+  const fp_t a0 = pr_dpp<DPP_EVEN>(a.v);
+  const fp_t a1 = pr_dpp<DPP_ODD>(a.v);
+  if (fp_is_zero(a1)) {
+    // even lane: sqrt(a0) -> (s, 0);  odd lane: sqrt(-a0) -> (0, s)
+    fp_t s;
+    const bool ok = fp_sqrt(s, odd ? fp_neg(a0) : a0);
+    const bool ok0 = pr_dpp<DPP_EVEN>((uint32_t)ok) != 0;
+    const bool ok1 = pr_dpp<DPP_ODD>((uint32_t)ok) != 0;
+    if (ok0) { r.v = odd ? fp_zero() : s; return true; }
+    if (ok1) { r.v = odd ? s : fp_zero(); return true; }
+    return false;
+  }
+  const fp_t t2 = fp_sqr(a.v);
+  const fp_t alpha = fp_add(t2, pr_dpp<DPP_SWAP>(t2));
+  fp_t gamma;
+  if (!fp_sqrt(gamma, alpha)) return false;
+  const fp_t delta = fp_half(fp_add(a0, gamma));
+  const fp_t z = fp_pow_pair(delta, EXP_SQRT, EXP_ISQRT, EXP_ISQRT_BITS);
+  const fp_t t = pr_dpp<DPP_EVEN>(z);
+  const fp_t other = fp_mul(a1, fp_half(pr_dpp<DPP_ODD>(z)));
+  const bool sq = fp_eq(fp_sqr(t), delta);
+  r.v = (sq != odd) ? t : other;
+  return true;
+}
+
+// curve-generic helpers (bls381_curve.hpp) for the pair representation
+__device__ __forceinline__ fp2p_t f_add(const fp2p_t& a, const fp2p_t& b) { return fp2_add(a, b); }
+__device__ __forceinline__ fp2p_t f_sub(const fp2p_t& a, const fp2p_t& b) { return fp2_sub(a, b); }
+__device__ __forceinline__ fp2p_t f_mul(const fp2p_t& a, const fp2p_t& b) { return fp2_mul(a, b); }
+__device__ __forceinline__ fp2p_t f_sqr(const fp2p_t& a) { return fp2_sqr(a); }
+__device__ __forceinline__ fp2p_t f_dbl(const fp2p_t& a) { return fp2_dbl(a); }
+__device__ __forceinline__ fp2p_t f_neg(const fp2p_t& a) { return fp2_neg(a); }
+__device__ __forceinline__ bool f_is_zero(const fp2p_t& a) { return fp2_is_zero(a); }
+__device__ __forceinline__ bool f_eq(const fp2p_t& a, const fp2p_t& b) { return fp2_eq(a, b); }
+__device__ __forceinline__ fp2p_t f_inv(const fp2p_t& a) { return fp2_inv(a); }
+__device__ __forceinline__ void f_set_zero(fp2p_t& a) { a = e2_zero<fp2p_t>(); }
+__device__ __forceinline__ void f_set_one(fp2p_t& a) { a = e2_one<fp2p_t>(); }
+
+// --------------------------------------------------------------- G2 codec --
+// a_flag rule of py_ecc compress/decompress_G2: from y_im, or y_re if y_im == 0
+__device__ __forceinline__ int g2_y_flag(const fp2p_t& y_mont) {
+  const fp_t yc = fp_from_mont(y_mont.v);
+  const uint32_t up = fp_plain_is_upper_half(yc) ? 1u : 0u;
+  const uint32_t z = fp_is_zero(yc) ? 1u : 0u;
+  const uint32_t up0 = pr_dpp<DPP_EVEN>(up), up1 = pr_dpp<DPP_ODD>(up), z1 = pr_dpp<DPP_ODD>(z);
+  return (int)(z1 ? up0 : up1);
+}
+
+// G2 decompress (bls_signature.md:54-64): z1 = flags | x_im (odd lane), z2 = x_re (even lane)
+__device__ inline int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96) {
+  const bool odd = pr_odd();
+  const uint8_t top = b96[0];
+  const int c1 = (top >> 7) & 1, b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
+  if (b96[48] & 0xe0) return PT_BAD;      // a_flag2 == b_flag2 == c_flag2 == 0
+  uint8_t tmp[48];
+  const uint8_t* src = b96 + (odd ? 0 : 48);
+  for (int i = 0; i < 48; ++i) tmp[i] = src[i];
+  if (odd) tmp[0] &= 0x1f;
+  const fp_t xc = fp_plain_from_be48(tmp);
+  if (!c1) return PT_BAD;
+  if (b1) return (a1 == 0 && pr_both(fp_is_zero(xc))) ? PT_INF : PT_BAD;
+  if (!pr_both(fp_plain_lt_q(xc))) return PT_BAD;
+  fp2p_t x;
+  x.v = fp_to_mont(xc);
+  const fp2p_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
+  fp2p_t y;
+  if (!fp2_sqrt(y, rhs)) return PT_BAD;
+  if (g2_y_flag(y) != a1) y = fp2_neg(y);
+  out.x = x;
+  out.y = y;
+  return PT_OK;
+}
+
+// each lane writes its 48-byte half of the 96-byte encoding at out96
+__device__ inline void g2_compress_aff(uint8_t* out96, const aff_t<fp2p_t>& a) {
+  const bool odd = pr_odd();
+  const int flag = g2_y_flag(a.y);
+  uint8_t b[48];
+  fp_plain_to_be48(b, fp_from_mont(a.x.v));
+  if (odd) b[0] |= 0x80 | (flag ? 0x20 : 0);
+  uint8_t* dst = out96 + (odd ? 0 : 48);
+  for (int i = 0; i < 48; ++i) dst[i] = b[i];
+}
+
+__device__ inline void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
+  aff_t<fp2p_t> a;
+  if (!jac_to_aff(a, p)) {
+    const bool odd = pr_odd();
+    uint8_t* dst = out96 + (odd ? 0 : 48);
+    for (int i = 0; i < 48; ++i) dst[i] = 0;
+    if (odd) dst[0] = 0xc0;
+    return;
+  }
+  g2_compress_aff(out96, a);
+}
+
+// ------------------------------------------------------------ hash_to_G2 --
+// try-and-increment (bls_signature.md:74-86) before the cofactor: the even lane
+// hashes m || dom8 || 0x01 (x_re), the odd lane m || dom8 || 0x02 (x_im).
+__device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* msg, uint32_t mlen,
+                                           const uint8_t dom8[8], uint8_t* scratch /* mlen + 9 */) {
+  const bool odd = pr_odd();
+  for (uint32_t i = 0; i < mlen; ++i) scratch[i] = msg[i];
+  for (int i = 0; i < 8; ++i) scratch[mlen + i] = dom8[i];
+  scratch[mlen + 8] = odd ? 2 : 1;
+  uint32_t d[8];
+  sha256(d, scratch, mlen + 9);
+  fp2p_t x;
+  x.v = fp_to_mont(fp_plain_from_digest(d));
+  const fp_t inc = fp_sel(odd, fp_zero(), FP_ONE_M);   // x += 1 (real part)
+  int trials = 0;
+  while (true) {
+    ++trials;
+    const fp2p_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
+    fp2p_t y;
+    if (fp2_sqrt(y, rhs)) {
+      out.x = x;
+      out.y = g2_select_root(y);
+      return trials;
+    }
+    x.v = fp_add(x.v, inc);
+  }
+}
+
+}  // namespace bls381

@@ -31,30 +31,32 @@ BLS_INLINE g1_line_pre g1_prepare(const aff_t<fp_t>& p) {
 }
 
 // homogeneous-projective T on E'(Fp2)
-struct g2_proj { fp2_t x, y, z; };
+template <class E> struct g2_proj { E x, y, z; };
 
-BLS_INLINE fp2_t fp2_mul_b(const fp2_t& a) {
+template <class E>
+BLS_INLINE E fp2_mul_b(const E& a) {
   // b' = 4(1+u): a * b' = 4 * xi * a
-  const fp2_t t = fp2_mul_xi(a);
+  const E t = fp2_mul_xi(a);
   return fp2_dbl(fp2_dbl(t));
 }
 
 // doubling step: T <- 2T, returns the tangent line at the old T evaluated at P
-BLS_HD inline void line_dbl(g2_proj& T, const g1_line_pre& P, fp2_t& c0, fp2_t& c1, fp2_t& c2) {
-  const fp2_t XX = fp2_sqr(T.x);
-  const fp2_t YY = fp2_sqr(T.y);
-  const fp2_t ZZ = fp2_sqr(T.z);
-  const fp2_t YZ = fp2_mul(T.y, T.z);
-  const fp2_t bZZ = fp2_mul_b(ZZ);
-  const fp2_t b3 = fp2_add(fp2_dbl(bZZ), bZZ);        // 3 b' Z^2
-  const fp2_t b9 = fp2_add(fp2_dbl(b3), b3);          // 9 b' Z^2
+template <class E>
+BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E& c2) {
+  const E XX = fp2_sqr(T.x);
+  const E YY = fp2_sqr(T.y);
+  const E ZZ = fp2_sqr(T.z);
+  const E YZ = fp2_mul(T.y, T.z);
+  const E bZZ = fp2_mul_b(ZZ);
+  const E b3 = fp2_add(fp2_dbl(bZZ), bZZ);        // 3 b' Z^2
+  const E b9 = fp2_add(fp2_dbl(b3), b3);          // 9 b' Z^2
   c0 = fp2_sub(YY, b3);
   c1 = fp2_mul_fp(XX, P.n3x);
   c2 = fp2_mul_fp(YZ, P.y2);
-  const fp2_t XY = fp2_mul(T.x, T.y);
-  const fp2_t h = fp2_half(fp2_add(YY, b9));
-  const fp2_t b3sq = fp2_sqr(b3);                      // 9 b'^2 Z^4
-  g2_proj R;
+  const E XY = fp2_mul(T.x, T.y);
+  const E h = fp2_half(fp2_add(YY, b9));
+  const E b3sq = fp2_sqr(b3);                      // 9 b'^2 Z^4
+  g2_proj<E> R;
   R.x = fp2_half(fp2_mul(XY, fp2_sub(YY, b9)));
   R.y = fp2_sub(fp2_sqr(h), fp2_add(fp2_dbl(b3sq), b3sq));  // h^2 - 27 b'^2 Z^4
   R.z = fp2_dbl(fp2_mul(YY, YZ));
@@ -62,18 +64,18 @@ BLS_HD inline void line_dbl(g2_proj& T, const g1_line_pre& P, fp2_t& c0, fp2_t& 
 }
 
 // addition step: T <- T + Q, returns the chord through T and Q evaluated at P
-BLS_HD inline void line_add(g2_proj& T, const aff_t<fp2_t>& Q, const g1_line_pre& P,
-                            fp2_t& c0, fp2_t& c1, fp2_t& c2) {
-  const fp2_t u = fp2_sub(fp2_mul(Q.y, T.z), T.y);
-  const fp2_t v = fp2_sub(fp2_mul(Q.x, T.z), T.x);
+template <class E>
+BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre& P, E& c0, E& c1, E& c2) {
+  const E u = fp2_sub(fp2_mul(Q.y, T.z), T.y);
+  const E v = fp2_sub(fp2_mul(Q.x, T.z), T.x);
   c0 = fp2_sub(fp2_mul(u, Q.x), fp2_mul(v, Q.y));
   c1 = fp2_mul_fp(u, P.nx);
   c2 = fp2_mul_fp(v, P.y);
-  const fp2_t vv = fp2_sqr(v);
-  const fp2_t vvv = fp2_mul(vv, v);
-  const fp2_t vvX = fp2_mul(vv, T.x);
-  const fp2_t A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(u), T.z), vvv), fp2_dbl(vvX));
-  g2_proj R;
+  const E vv = fp2_sqr(v);
+  const E vvv = fp2_mul(vv, v);
+  const E vvX = fp2_mul(vv, T.x);
+  const E A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(u), T.z), vvv), fp2_dbl(vvX));
+  g2_proj<E> R;
   R.x = fp2_mul(v, A);
   R.y = fp2_sub(fp2_mul(u, fp2_sub(vvX, A)), fp2_mul(vvv, T.y));
   R.z = fp2_mul(vvv, T.z);
@@ -83,23 +85,23 @@ BLS_HD inline void line_add(g2_proj& T, const aff_t<fp2_t>& Q, const g1_line_pre
 // Multi-Miller loop over n pairs (Q_k affine in G2, P_k affine in G1), all finite.
 // Returns conj(prod_k f_{|x|,Q_k}(P_k)) = prod_k f_{x,Q_k}(P_k) up to factors the
 // final exponentiation removes.  Squarings of f are shared by all pairs.
-template <int N>
-BLS_HD inline fp12_t miller_loop_n(const aff_t<fp2_t>* Q, const g1_line_pre* P) {
-  g2_proj T[N];
-  for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = fp2_one(); }
-  fp12_t f = fp12_one();
+template <int N, class E>
+BLS_HD inline fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P) {
+  g2_proj<E> T[N];
+  for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = e2_one<E>(); }
+  fp12_g<E> f = fp12_one<E>();
   bool first = true;
   for (int i = 62; i >= 0; --i) {
     if (!first) f = fp12_sqr(f);
     for (int k = 0; k < N; ++k) {
-      fp2_t c0, c1, c2;
+      E c0, c1, c2;
       line_dbl(T[k], P[k], c0, c1, c2);
       f = fp12_mul_by_line(f, c0, c1, c2);
     }
     first = false;
     if ((BLS_X_ABS >> i) & 1) {
       for (int k = 0; k < N; ++k) {
-        fp2_t c0, c1, c2;
+        E c0, c1, c2;
         line_add(T[k], Q[k], P[k], c0, c1, c2);
         f = fp12_mul_by_line(f, c0, c1, c2);
       }
@@ -109,13 +111,15 @@ BLS_HD inline fp12_t miller_loop_n(const aff_t<fp2_t>* Q, const g1_line_pre* P) 
 }
 
 // runtime pair count (for verify_multiple chunks); pairs processed one at a time
-BLS_HD inline fp12_t miller_loop_1(const aff_t<fp2_t>& Q, const g1_line_pre& P) {
+template <class E>
+BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P) {
   return miller_loop_n<1>(&Q, &P);
 }
 
 // f^|x| in the cyclotomic subgroup, then conjugate for x < 0
-BLS_HD inline fp12_t cyc_exp_x(const fp12_t& f) {
-  fp12_t r = f;
+template <class E>
+BLS_HD inline fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+  fp12_g<E> r = f;
   for (int i = 62; i >= 0; --i) {
     r = fp12_cyclotomic_sqr(r);
     if ((BLS_X_ABS >> i) & 1) r = fp12_mul(r, f);
@@ -126,15 +130,16 @@ BLS_HD inline fp12_t cyc_exp_x(const fp12_t& f) {
 // f^(3 (q^12 - 1)/r).  3 is coprime to r, so the result is 1 exactly when the
 // reduced pairing value is 1 (DESIGN.md "Final exponentiation").
 // Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3.
-BLS_HD inline fp12_t final_exp(const fp12_t& f) {
-  fp12_t t = fp12_mul(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
+template <class E>
+BLS_HD inline fp12_g<E> final_exp(const fp12_g<E>& f) {
+  fp12_g<E> t = fp12_mul(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
   t = fp12_mul(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
-  fp12_t a = fp12_mul(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
+  fp12_g<E> a = fp12_mul(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
   a = fp12_mul(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
-  const fp12_t b = fp12_mul(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
-  const fp12_t bx2 = cyc_exp_x(cyc_exp_x(b));
-  const fp12_t c = fp12_mul(fp12_mul(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
-  const fp12_t t3 = fp12_mul(fp12_cyclotomic_sqr(t), t);
+  const fp12_g<E> b = fp12_mul(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
+  const fp12_g<E> bx2 = cyc_exp_x(cyc_exp_x(b));
+  const fp12_g<E> c = fp12_mul(fp12_mul(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
+  const fp12_g<E> t3 = fp12_mul(fp12_cyclotomic_sqr(t), t);
   return fp12_mul(c, t3);
 }
 

@@ -21,7 +21,7 @@ def main():
     from bls381_amd import _native as native
     native.init(0)
     L = native.lib()
-    pks, msgs, sigs, doms, expected = bench.make_workload(native, n, 0xB15_0001)
+    pks, msgs, sigs, doms, expected, _ = bench.make_workload(native, n, 0xB15_0001)
     dev = torch.device("cuda", 0)
     t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
     d = [t(pks), t(msgs), t(sigs), t(doms)]
