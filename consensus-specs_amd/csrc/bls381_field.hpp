@@ -236,11 +236,37 @@ BLS_HD inline fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
   return r;
 }
 
-BLS_HD inline fp_t fp_inv(const fp_t& a) { return fp_pow_limbs(a, EXP_INV, 381); }
+// u = a^((q-3)/4) by a 4-bit sliding window over the generated schedule
+// (375 squarings + 78 multiplications + 8 for the odd-power table, against 605
+// for plain square-and-multiply).  Every square root and inversion is built
+// from this one power: sqrt(a) = u a, 1/a = u^4 a, 1/sqrt(a) = u^3 a.
+BLS_HD inline fp_t fp_pow_qm3d4(const fp_t& a) {
+  const fp_t a2 = fp_sqr(a);
+  const fp_t t1 = a, t3 = fp_mul(t1, a2), t5 = fp_mul(t3, a2), t7 = fp_mul(t5, a2);
+  const fp_t t9 = fp_mul(t7, a2), t11 = fp_mul(t9, a2), t13 = fp_mul(t11, a2), t15 = fp_mul(t13, a2);
+  fp_t r = FP_ONE_M;
+  for (int k = 0; k < POW_QM3D4_NSTEPS; ++k) {
+    for (int j = POW_QM3D4_SQR[k]; j > 0; --j) r = fp_sqr(r);
+    switch (POW_QM3D4_DIG[k]) {   // uniform digit: a scalar branch, the table stays in registers
+      case 1: r = fp_mul(r, t1); break;
+      case 3: r = fp_mul(r, t3); break;
+      case 5: r = fp_mul(r, t5); break;
+      case 7: r = fp_mul(r, t7); break;
+      case 9: r = fp_mul(r, t9); break;
+      case 11: r = fp_mul(r, t11); break;
+      case 13: r = fp_mul(r, t13); break;
+      case 15: r = fp_mul(r, t15); break;
+      default: break;
+    }
+  }
+  return r;
+}
+
+BLS_HD inline fp_t fp_inv(const fp_t& a) { return fp_mul(fp_sqr(fp_sqr(fp_pow_qm3d4(a))), a); }
 
 // returns true and sets r when a is a square; r = a^((q+1)/4)
 BLS_HD inline bool fp_sqrt(fp_t& r, const fp_t& a) {
-  r = fp_pow_limbs(a, EXP_SQRT, 379);
+  r = fp_mul(fp_pow_qm3d4(a), a);
   return fp_eq(fp_sqr(r), a);
 }
 
@@ -314,6 +340,80 @@ BLS_INLINE void fp_plain_to_be48(uint8_t* p, const fp_t& a) {
     b[2] = (uint8_t)(w >> 8);
     b[3] = (uint8_t)w;
   }
+}
+
+// plain canonical value -> 12 little-endian u32 words
+BLS_INLINE void fp_plain_to_words(uint32_t w[12], const fp_t& a) {
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const int bit = 32 * i, k = bit / 28, sh = bit % 28;
+    uint64_t v = (uint64_t)a.w[k] >> sh;
+    if (k + 1 < 14) v |= (uint64_t)a.w[k + 1] << (28 - sh);
+    if (k + 2 < 14 && 56 - sh < 32) v |= (uint64_t)a.w[k + 2] << (56 - sh);
+    w[i] = (uint32_t)v;
+  }
+}
+
+// Legendre symbol (a/q) of a Montgomery-form a: 1 (nonzero square), -1
+// (non-square) or 0.  Binary Jacobi algorithm on 12 x 32-bit words: about 270
+// subtract-and-shift steps of ~60 word ops each, an order of magnitude cheaper
+// than Euler's criterion a^((q-1)/2), so the try-and-increment loop of
+// hash_to_G2 pays a full square root only for the candidate that succeeds.
+BLS_HD inline int fp_legendre(const fp_t& am) {
+  uint32_t a[12], n[12];
+  fp_plain_to_words(a, fp_from_mont(am));
+  fp_plain_to_words(n, FP_Q_PLAIN);
+  uint32_t t = 0;   // accumulated sign flips
+  while (true) {
+    uint32_t z = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) z |= a[i];
+    if (z == 0) break;
+    // remove factors of two; (2/n) = -1 iff n = 3, 5 mod 8
+    const uint32_t n8 = n[0] & 7u;
+    const uint32_t flip2 = (n8 == 3u || n8 == 5u) ? 1u : 0u;
+    while ((a[0] & 1u) == 0) {
+      if (a[0] == 0) {
+#pragma unroll
+        for (int i = 0; i < 11; ++i) a[i] = a[i + 1];
+        a[11] = 0;
+        continue;
+      }
+      const uint32_t k = (uint32_t)__builtin_ctz(a[0]);
+#pragma unroll
+      for (int i = 0; i < 11; ++i) a[i] = (a[i] >> k) | (a[i + 1] << (32 - k));
+      a[11] >>= k;
+      t ^= (k & 1u) & flip2;
+    }
+    // a, n odd: d = a - n; if a < n swap (reciprocity flip when both are 3 mod 4), a = |a - n|
+    uint32_t d[12];
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const uint64_t v = (uint64_t)a[i] - n[i] - br;
+      d[i] = (uint32_t)v;
+      br = (uint32_t)(v >> 63);
+    }
+    if (br) {
+      t ^= (a[0] & n[0] & 2u) >> 1;
+      uint32_t nb = 0;
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        n[i] = a[i];
+        const uint64_t v = (uint64_t)0 - d[i] - nb;
+        a[i] = (uint32_t)v;
+        nb = (uint32_t)(v >> 63);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 12; ++i) a[i] = d[i];
+    }
+  }
+  uint32_t one = n[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < 12; ++i) one |= n[i];
+  if (one != 0) return 0;
+  return t ? -1 : 1;
 }
 
 // ---------------------------------------------------------------- Fp2 -----
@@ -441,9 +541,11 @@ BLS_HD inline bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   fp_t gamma;
   if (!fp_sqrt(gamma, alpha)) return false;
   const fp_t delta = fp_half(fp_add(a.c0, gamma));
-  const fp_t t = fp_pow_limbs(delta, EXP_SQRT, 379);
-  const fp_t inv2t = fp_inv(fp_dbl(t));
-  const fp_t other = fp_mul(a.c1, inv2t);
+  // t = delta^((q+1)/4) and 1/t = delta^((3q-5)/4) from one power u = delta^((q-3)/4):
+  // t = u delta, 1/t = u^2 t (delta != 0 here because a1 != 0)
+  const fp_t u = fp_pow_qm3d4(delta);
+  const fp_t t = fp_mul(u, delta);
+  const fp_t other = fp_mul(a.c1, fp_half(fp_mul(fp_sqr(u), t)));   // a1 / (2t)
   if (fp_eq(fp_sqr(t), delta)) { r.c0 = t; r.c1 = other; }
   else { r.c0 = other; r.c1 = t; }
   return true;

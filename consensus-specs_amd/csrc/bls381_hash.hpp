@@ -102,7 +102,9 @@ BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, ui
     ++trials;
     const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
     fp2_t y;
-    if (fp2_sqrt(y, rhs)) {
+    // rhs is a square in Fp2 iff its norm is a square in Fp: a cheap Legendre
+    // test rejects non-squares before the square root's exponentiations
+    if (fp_legendre(fp_add(fp_sqr(rhs.c0), fp_sqr(rhs.c1))) >= 0 && fp2_sqrt(y, rhs)) {
       out.x = x;
       out.y = g2_select_root(y);
       return trials;

@@ -76,19 +76,6 @@ __device__ __forceinline__ fp_t fp_addsub(const fp_t& a, const fp_t& b, bool add
   return r;
 }
 
-// r = base^e with a per-lane exponent: even lanes use ea, odd lanes eb (nbits
-// covers both).  The multiply runs when either lane of the pair needs it.
-__device__ inline fp_t fp_pow_pair(const fp_t& base, const uint32_t* ea, const uint32_t* eb, int nbits) {
-  const bool odd = pr_odd();
-  fp_t r = FP_ONE_M;
-  for (int i = nbits - 1; i >= 0; --i) {
-    r = fp_sqr(r);
-    const uint32_t w = odd ? eb[i >> 5] : ea[i >> 5];
-    if ((w >> (i & 31)) & 1u) r = fp_mul(r, base);
-  }
-  return r;
-}
-
 // ------------------------------------------------------ Fp2 multiplication --
 // lane 0: a0 b0 + a1 (8q - b1) = Re(ab);  lane 1: a1 b0 + a0 b1 = Im(ab).
 // Operands may be lazy sums (limbs < 2^29, values < 4q).  Column k holds <= 14
@@ -170,11 +157,11 @@ __device__ inline fp2p_t fp2_inv(const fp2p_t& a) {
   return pr_make(fp_sel(pr_odd(), fp_neg(r), r));
 }
 
-// Complex-method square root (same root set as the one-lane fp2_sqrt, so the
+// Complex-method square root (same steps as the one-lane fp2_sqrt, so the
 // spec's selection rule picks the same root).  With gamma = sqrt(a0^2 + a1^2)
-// and delta = (a0 + gamma)/2, the even lane raises delta to (q+1)/4 (= t) while
-// the odd lane raises it to (3q-5)/4 (= 1/t) in the same loop; the root is
-// (t, a1/(2t)) when t^2 = delta and (a1/(2t), t) otherwise.
+// and delta = (a0 + gamma)/2 (both lanes), t = delta^((q+1)/4) and 1/t come
+// from one power of delta; the root is (t, a1/(2t)) when t^2 = delta and
+// (a1/(2t), t) otherwise.
 __device__ inline bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
   const bool odd = pr_odd();
   const fp_t a0 = pr_dpp<DPP_EVEN>(a.v);
@@ -194,9 +181,9 @@ __device__ inline bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
   fp_t gamma;
   if (!fp_sqrt(gamma, alpha)) return false;
   const fp_t delta = fp_half(fp_add(a0, gamma));
-  const fp_t z = fp_pow_pair(delta, EXP_SQRT, EXP_ISQRT, EXP_ISQRT_BITS);
-  const fp_t t = pr_dpp<DPP_EVEN>(z);
-  const fp_t other = fp_mul(a1, fp_half(pr_dpp<DPP_ODD>(z)));
+  const fp_t u = fp_pow_qm3d4(delta);
+  const fp_t t = fp_mul(u, delta);                                   // delta^((q+1)/4)
+  const fp_t other = fp_mul(a1, fp_half(fp_mul(fp_sqr(u), t)));     // a1 / (2t)
   const bool sq = fp_eq(fp_sqr(t), delta);
   r.v = (sq != odd) ? t : other;
   return true;
@@ -292,7 +279,10 @@ __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* ms
     ++trials;
     const fp2p_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
     fp2p_t y;
-    if (fp2_sqrt(y, rhs)) {
+    // square in Fp2 iff the norm is a square in Fp: the Legendre test (both
+    // lanes, same norm) rejects non-squares before the exponentiations
+    const fp_t t = fp_sqr(rhs.v);
+    if (fp_legendre(fp_add(t, pr_dpp<DPP_SWAP>(t))) >= 0 && fp2_sqrt(y, rhs)) {
       out.x = x;
       out.y = g2_select_root(y);
       return trials;

@@ -48,6 +48,7 @@ int hc_fp_sqrt(const uint8_t* a, uint8_t* o) {
   st(o, r);
   return ok;
 }
+int hc_fp_legendre(const uint8_t* a) { return fp_legendre(ld(a)); }
 // raw Montgomery multiply on plain limbs (checks fp_mul's bound handling directly)
 void hc_fp_mont_mul_raw(const uint8_t* a, const uint8_t* b, uint8_t* o) {
   fp_plain_to_be48(o, fp_mul(fp_plain_from_be48(a), fp_plain_from_be48(b)));

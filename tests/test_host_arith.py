@@ -51,6 +51,18 @@ def test_fp_ops(L):
         assert v < 2 * q and v % q == a * b * Rinv % q
 
 
+def test_fp_legendre(L):
+    """Binary-Jacobi Legendre symbol == Euler's criterion (squares, non-squares, 0, edges)."""
+    rng = random.Random(21)
+    L.hc_fp_legendre.restype = ctypes.c_int
+    vals = [0, 1, 2, 3, 4, q - 1, q - 2, (q - 1) // 2, 2 ** 255, 2 ** 380 + 5]
+    vals += [rng.randrange(q) for _ in range(300)] + [rng.randrange(q) ** 2 % q for _ in range(50)]
+    for a in vals:
+        e = pow(a, (q - 1) // 2, q)
+        want = 0 if a % q == 0 else (1 if e == 1 else -1)
+        assert L.hc_fp_legendre(b48(a)) == want, hex(a)
+
+
 def test_fp_mul_extreme_operands(L):
     """fp_mul accepts any operands with limbs < 2^28 and value < 2^384 (< 9.6q):
     output must stay < 2q and congruent (column sums stay < 2^64)."""
