@@ -573,7 +573,7 @@ template <class E> BLS_INLINE fp6_g<E> fp6_neg(const fp6_g<E>& a) { fp6_g<E> r; 
 template <class E> BLS_INLINE bool fp6_is_zero(const fp6_g<E>& a) { return fp2_is_zero(a.c0) && fp2_is_zero(a.c1) && fp2_is_zero(a.c2); }
 
 template <class E>
-BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) {
+BLS_INLINE fp6_g<E> fp6_mul_inl(const fp6_g<E>& a, const fp6_g<E>& b) {
   const E t0 = fp2_mul(a.c0, b.c0);
   const E t1 = fp2_mul(a.c1, b.c1);
   const E t2 = fp2_mul(a.c2, b.c2);
@@ -583,6 +583,9 @@ BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) {
   r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), fp2_add(t0, t2)), t1);
   return r;
 }
+
+template <class E>
+BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) { return fp6_mul_inl(a, b); }
 
 template <class E>
 BLS_INLINE fp6_g<E> fp6_mul_by_v(const fp6_g<E>& a) {
@@ -630,14 +633,17 @@ BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
 // complex squaring: (a + b w)^2 = (a^2 + v b^2) + 2ab w
 //   = ((a + b)(a + v b) - ab - v ab) + 2ab w
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_sqr(const fp12_g<E>& f) {
-  const fp6_g<E> ab = fp6_mul(f.c0, f.c1);
-  const fp6_g<E> t = fp6_mul(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
+BLS_INLINE fp12_g<E> fp12_sqr_inl(const fp12_g<E>& f) {
+  const fp6_g<E> ab = fp6_mul_inl(f.c0, f.c1);
+  const fp6_g<E> t = fp6_mul_inl(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
   fp12_g<E> r;
   r.c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_by_v(ab));
   r.c1 = fp6_add(ab, ab);
   return r;
 }
+
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_sqr(const fp12_g<E>& f) { return fp12_sqr_inl(f); }
 
 template <class E>
 BLS_INLINE fp12_g<E> fp12_conj(const fp12_g<E>& a) { fp12_g<E> r; r.c0 = a.c0; r.c1 = fp6_neg(a.c1); return r; }
@@ -673,7 +679,7 @@ BLS_HD inline fp12_g<E> fp12_frob(const fp12_g<E>& f, int p) {
 
 // sparse product f * (c0 + c1 v + c2 v w): 13 Fp2 multiplications
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E& c1, const E& c2) {
+BLS_INLINE fp12_g<E> fp12_mul_by_line_inl(const fp12_g<E>& f, const E& c0, const E& c1, const E& c2) {
   const fp6_g<E>& a = f.c0;
   const fp6_g<E>& b = f.c1;
   // aA, A = c0 + c1 v
@@ -705,6 +711,11 @@ BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E
   r.c0 = fp6_add(aA, fp6_mul_by_v(bB));
   r.c1 = fp6_sub(fp6_sub(m, aA), bB);
   return r;
+}
+
+template <class E>
+BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E& c1, const E& c2) {
+  return fp12_mul_by_line_inl(f, c0, c1, c2);
 }
 
 // Granger-Scott squaring in the cyclotomic subgroup.  View Fp12 as

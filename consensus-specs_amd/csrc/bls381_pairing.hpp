@@ -85,25 +85,27 @@ BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre&
 // Multi-Miller loop over n pairs (Q_k affine in G2, P_k affine in G1), all finite.
 // Returns conj(prod_k f_{|x|,Q_k}(P_k)) = prod_k f_{x,Q_k}(P_k) up to factors the
 // final exponentiation removes.  Squarings of f are shared by all pairs.
+// One function per pair count; inside it the Fp12 squaring and line products
+// are inlined so f stays in registers for the whole loop.
 template <int N, class E>
-BLS_HD inline fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P) {
+BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P) {
   g2_proj<E> T[N];
   for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = e2_one<E>(); }
   fp12_g<E> f = fp12_one<E>();
   bool first = true;
   for (int i = 62; i >= 0; --i) {
-    if (!first) f = fp12_sqr(f);
+    if (!first) f = fp12_sqr_inl(f);
     for (int k = 0; k < N; ++k) {
       E c0, c1, c2;
       line_dbl(T[k], P[k], c0, c1, c2);
-      f = fp12_mul_by_line(f, c0, c1, c2);
+      f = fp12_mul_by_line_inl(f, c0, c1, c2);
     }
     first = false;
     if ((BLS_X_ABS >> i) & 1) {
       for (int k = 0; k < N; ++k) {
         E c0, c1, c2;
         line_add(T[k], Q[k], P[k], c0, c1, c2);
-        f = fp12_mul_by_line(f, c0, c1, c2);
+        f = fp12_mul_by_line_inl(f, c0, c1, c2);
       }
     }
   }
@@ -117,11 +119,13 @@ BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P) {
 }
 
 // f^|x| in the cyclotomic subgroup, then conjugate for x < 0
+// One call per exponentiation: the 63 squarings are inlined so r stays in
+// registers across the loop (a call per squaring would pass r through scratch).
 template <class E>
-BLS_HD inline fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   fp12_g<E> r = f;
   for (int i = 62; i >= 0; --i) {
-    r = fp12_cyclotomic_sqr(r);
+    r = fp12_cyclotomic_sqr_inl(r);
     if ((BLS_X_ABS >> i) & 1) r = fp12_mul(r, f);
   }
   return fp12_conj(r);
