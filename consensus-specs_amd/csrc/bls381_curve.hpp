@@ -130,9 +130,11 @@ BLS_HD inline bool jac_to_aff(aff_t<F>& out, const jac_t<F>& p) {
   return true;
 }
 
+// Scalar multiplications are one (non-inlined) function each, with the point
+// formulas inlined into the loop, so the running point stays in registers.
 // [k] a for a 64-bit scalar, affine base, left-to-right
 template <class F>
-BLS_HD inline jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
+BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
   jac_t<F> r = jac_from_aff(a);
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -145,7 +147,7 @@ BLS_HD inline jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
 
 // [k] p for a 64-bit scalar, Jacobian base
 template <class F>
-BLS_HD inline jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {
+BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {
   jac_t<F> r = p;
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -158,7 +160,7 @@ BLS_HD inline jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {
 
 // [k] a for a little-endian multi-limb scalar (nbits significant bits)
 template <class F>
-BLS_HD inline jac_t<F> jac_mul_limbs(const aff_t<F>& a, const uint32_t* k, int nbits) {
+BLS_NOINLINE jac_t<F> jac_mul_limbs(const aff_t<F>& a, const uint32_t* k, int nbits) {
   jac_t<F> r = jac_infinity<F>();
   for (int i = nbits - 1; i >= 0; --i) {
     r = jac_dbl(r);

@@ -354,60 +354,77 @@ BLS_INLINE void fp_plain_to_words(uint32_t w[12], const fp_t& a) {
   }
 }
 
+// word-level borrow chain step: a - b - bin, borrow out
+BLS_INLINE uint32_t sub_borrow(uint32_t a, uint32_t b, uint32_t bin, uint32_t& bout) {
+#if defined(__clang__)
+  unsigned int bo;
+  const uint32_t r = __builtin_subc(a, b, bin, &bo);
+  bout = bo;
+  return r;
+#else
+  const uint64_t v = (uint64_t)a - b - bin;
+  bout = (uint32_t)(v >> 63);
+  return (uint32_t)v;
+#endif
+}
+
+// a >>= k (1 <= k <= 31) across 12 words; funnel shifts
+BLS_INLINE void words_shr(uint32_t a[12], uint32_t k) {
+#pragma unroll
+  for (int i = 0; i < 11; ++i) a[i] = (uint32_t)((((uint64_t)a[i + 1] << 32) | a[i]) >> k);
+  a[11] >>= k;
+}
+
+// strip the factors of two of a (a != 0); returns the parity of their number
+BLS_INLINE uint32_t words_strip_twos(uint32_t a[12]) {
+  uint32_t par = 0;
+  while (a[0] == 0) {   // a whole zero word: probability ~2^-32 per step
+#pragma unroll
+    for (int i = 0; i < 11; ++i) a[i] = a[i + 1];
+    a[11] = 0;
+  }
+  const uint32_t k = (uint32_t)__builtin_ctz(a[0]);
+  if (k) {
+    words_shr(a, k);
+    par = k & 1u;
+  }
+  return par;
+}
+
 // Legendre symbol (a/q) of a Montgomery-form a: 1 (nonzero square), -1
-// (non-square) or 0.  Binary Jacobi algorithm on 12 x 32-bit words: about 270
-// subtract-and-shift steps of ~60 word ops each, an order of magnitude cheaper
-// than Euler's criterion a^((q-1)/2), so the try-and-increment loop of
-// hash_to_G2 pays a full square root only for the candidate that succeeds.
+// (non-square) or 0.  Binary Jacobi algorithm on 12 x 32-bit words, written
+// branch-free per step (one subtraction, a conditional swap via the sign, one
+// funnel shift): about 270 steps of ~80 word ops, an order of magnitude below
+// Euler's criterion a^((q-1)/2), so the try-and-increment loop of hash_to_G2
+// pays a full square root only for the candidate that succeeds.
 BLS_HD inline int fp_legendre(const fp_t& am) {
   uint32_t a[12], n[12];
   fp_plain_to_words(a, fp_from_mont(am));
   fp_plain_to_words(n, FP_Q_PLAIN);
-  uint32_t t = 0;   // accumulated sign flips
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) z |= a[i];
+  if (z == 0) return 0;
+  // (2/n) = -1 iff n = 3, 5 mod 8 (n = q here)
+  uint32_t t = words_strip_twos(a) & (((n[0] & 7u) == 3u || (n[0] & 7u) == 5u) ? 1u : 0u);
   while (true) {
-    uint32_t z = 0;
+    // a, n odd: d = a - n; when a < n swap (reciprocity: flip if both are 3 mod 4)
+    uint32_t d[12], br = 0;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) z |= a[i];
-    if (z == 0) break;
-    // remove factors of two; (2/n) = -1 iff n = 3, 5 mod 8
-    const uint32_t n8 = n[0] & 7u;
-    const uint32_t flip2 = (n8 == 3u || n8 == 5u) ? 1u : 0u;
-    while ((a[0] & 1u) == 0) {
-      if (a[0] == 0) {
-#pragma unroll
-        for (int i = 0; i < 11; ++i) a[i] = a[i + 1];
-        a[11] = 0;
-        continue;
-      }
-      const uint32_t k = (uint32_t)__builtin_ctz(a[0]);
-#pragma unroll
-      for (int i = 0; i < 11; ++i) a[i] = (a[i] >> k) | (a[i + 1] << (32 - k));
-      a[11] >>= k;
-      t ^= (k & 1u) & flip2;
-    }
-    // a, n odd: d = a - n; if a < n swap (reciprocity flip when both are 3 mod 4), a = |a - n|
-    uint32_t d[12];
-    uint32_t br = 0;
+    for (int i = 0; i < 12; ++i) d[i] = sub_borrow(a[i], n[i], br, br);
+    t ^= br & ((a[0] & n[0] & 2u) >> 1);
+    uint32_t nb = 0, nz = 0;
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
-      const uint64_t v = (uint64_t)a[i] - n[i] - br;
-      d[i] = (uint32_t)v;
-      br = (uint32_t)(v >> 63);
+      const uint32_t nd = sub_borrow(0u, d[i], nb, nb);   // |a - n| when a < n
+      const uint32_t an = a[i];
+      a[i] = br ? nd : d[i];
+      n[i] = br ? an : n[i];
+      nz |= a[i];
     }
-    if (br) {
-      t ^= (a[0] & n[0] & 2u) >> 1;
-      uint32_t nb = 0;
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        n[i] = a[i];
-        const uint64_t v = (uint64_t)0 - d[i] - nb;
-        a[i] = (uint32_t)v;
-        nb = (uint32_t)(v >> 63);
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 12; ++i) a[i] = d[i];
-    }
+    if (nz == 0) break;                                   // a == n: n = gcd
+    const uint32_t n8 = n[0] & 7u;
+    t ^= words_strip_twos(a) & ((n8 == 3u || n8 == 5u) ? 1u : 0u);
   }
   uint32_t one = n[0] ^ 1u;
 #pragma unroll

@@ -97,20 +97,21 @@ BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, ui
   scratch[mlen + 8] = 2;
   sha256(d, scratch, mlen + 9);
   x.c1 = fp_to_mont(fp_plain_from_digest(d));
+  // rhs is a square in Fp2 iff its norm is a square in Fp: the cheap Legendre
+  // test finds the candidate, then one square root is taken
   int trials = 0;
+  fp2_t rhs;
   while (true) {
     ++trials;
-    const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
-    fp2_t y;
-    // rhs is a square in Fp2 iff its norm is a square in Fp: a cheap Legendre
-    // test rejects non-squares before the square root's exponentiations
-    if (fp_legendre(fp_add(fp_sqr(rhs.c0), fp_sqr(rhs.c1))) >= 0 && fp2_sqrt(y, rhs)) {
-      out.x = x;
-      out.y = g2_select_root(y);
-      return trials;
-    }
+    rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
+    if (fp_legendre(fp_add(fp_sqr(rhs.c0), fp_sqr(rhs.c1))) >= 0) break;
     x.c0 = fp_add(x.c0, FP_ONE_M);
   }
+  fp2_t y;
+  fp2_sqrt(y, rhs);   // succeeds: rhs is a square
+  out.x = x;
+  out.y = g2_select_root(y);
+  return trials;
 }
 
 // psi on Jacobian coordinates: (cx conj(X), cy conj(Y), conj(Z))
@@ -133,8 +134,22 @@ BLS_INLINE jac_t<E> g2_psi_jac(const jac_t<E>& p) {
 //   Q_i = (-psi)^i BP(P).
 // ~190 doublings + ~45 additions instead of the 508-doubling ladder; the
 // identity is checked in oracle/tower_model.py and tests/test_tower_model.py.
+// [e0] S by the NAF of e0 (leading digit +1); one call, loop body inlined
 template <class E>
-BLS_HD inline jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
+BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E>& S) {
+  const jac_t<E> nS = jac_neg(S);
+  jac_t<E> R = S;
+  for (int i = 1; i < E0_NAF_LEN; ++i) {
+    R = jac_dbl(R);
+    const int dg = E0_NAF[i];
+    if (dg > 0) R = jac_add(R, S);
+    else if (dg < 0) R = jac_add(R, nS);
+  }
+  return R;
+}
+
+template <class E>
+BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
   aff_t<E> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
@@ -146,15 +161,7 @@ BLS_HD inline jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
   const jac_t<E> Q2 = jac_neg(g2_psi_jac(Q1));
   const jac_t<E> T = jac_add(jac_add(jac_dbl(Q2), Q1), jac_neg(g2_psi_jac(Q2)));   // Q1 + 2Q2 + Q3
   const jac_t<E> S = jac_add(jac_add(T, Q1), Q0);
-  const jac_t<E> nS = jac_neg(S);
-  jac_t<E> R = S;   // leading NAF digit of e0 is +1
-  for (int i = 1; i < E0_NAF_LEN; ++i) {
-    R = jac_dbl(R);
-    const int dg = E0_NAF[i];
-    if (dg > 0) R = jac_add(R, S);
-    else if (dg < 0) R = jac_add(R, nS);
-  }
-  return jac_add(R, jac_neg(T));
+  return jac_add(g2_mul_e0(S), jac_neg(T));
 }
 
 // full hash_to_G2 for a 32-byte message; returns false only if the result is infinity

@@ -274,21 +274,24 @@ __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* ms
   fp2p_t x;
   x.v = fp_to_mont(fp_plain_from_digest(d));
   const fp_t inc = fp_sel(odd, fp_zero(), FP_ONE_M);   // x += 1 (real part)
+  // Search with the cheap Legendre test only, then take one square root after
+  // the loop: inside the loop the root's exponentiations would run (under a
+  // partial exec mask) in every trial in which any lane of the wave succeeds.
+  // rhs is a square in Fp2 iff its norm is a square in Fp (both lanes, same norm).
   int trials = 0;
+  fp2p_t rhs;
   while (true) {
     ++trials;
-    const fp2p_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
-    fp2p_t y;
-    // square in Fp2 iff the norm is a square in Fp: the Legendre test (both
-    // lanes, same norm) rejects non-squares before the exponentiations
+    rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
     const fp_t t = fp_sqr(rhs.v);
-    if (fp_legendre(fp_add(t, pr_dpp<DPP_SWAP>(t))) >= 0 && fp2_sqrt(y, rhs)) {
-      out.x = x;
-      out.y = g2_select_root(y);
-      return trials;
-    }
+    if (fp_legendre(fp_add(t, pr_dpp<DPP_SWAP>(t))) >= 0) break;
     x.v = fp_add(x.v, inc);
   }
+  fp2p_t y;
+  fp2_sqrt(y, rhs);   // succeeds: rhs is a square
+  out.x = x;
+  out.y = g2_select_root(y);
+  return trials;
 }
 
 }  // namespace bls381
