@@ -38,6 +38,10 @@ struct Keep {
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  // side stream + fork/join events: independent stages of one batch run concurrently
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  std::mutex fork_mu;
   void* ws = nullptr;
   size_t ws_cap = 0;
   std::mutex mu;
@@ -91,7 +95,10 @@ Ctx* get_ctx(int* rc) {
     }
     Ctx* c = new Ctx();
     c->device = dev;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
       delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
     }
     g_ctx[dev] = c;
@@ -197,13 +204,20 @@ VerifyWs carve_verify(void* ws, size_t n) {
   return w;
 }
 
-int run_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs, const uint8_t* doms,
-                     uint8_t* verdicts, void* ws, hipStream_t s) {
+int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
+                     const uint8_t* doms, uint8_t* verdicts, void* ws, hipStream_t s) {
   VerifyWs w = carve_verify(ws, n);
   const dim3 g(grid_for(n)), g2(grid_for(2 * n)), b(KBLOCK);   // G1: lane per item; G2/Fp12: lane pair
-  LAUNCH("decode_g1", s, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
+  std::lock_guard<std::mutex> lk(c->fork_mu);
+  // decode_g1 (one lane per item: one wave per SIMD) on the side stream, beside
+  // decode_g2 and hash_to_g2; the Miller loop waits for both branches
+  HIPC(hipEventRecord(c->ev_fork, s));
+  HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
+  HIPC(hipEventRecord(c->ev_join, c->side));
   LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
          (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
   LAUNCH("final_exp", s, g2, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
@@ -523,6 +537,10 @@ void bls381_shutdown(void) {
     c->keep.clear();
     if (c->ws) (void)hipFree(c->ws);
     (void)hipStreamDestroy(c->stream);
+    (void)hipStreamSynchronize(c->side);
+    (void)hipStreamDestroy(c->side);
+    (void)hipEventDestroy(c->ev_fork);
+    (void)hipEventDestroy(c->ev_join);
     delete c;
   }
   g_ctx.clear();
@@ -577,7 +595,7 @@ int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_
   if (n == 0) return 0;
   if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace) return BLS381_EARG;
   hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream (torch's default stream)
-  return run_verify_batch(n, d_pks, d_msgs32, d_sigs, d_dom8s, d_verdicts, d_workspace, s);
+  return run_verify_batch(c, n, d_pks, d_msgs32, d_sigs, d_dom8s, d_verdicts, d_workspace, s);
 }
 
 int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
@@ -602,7 +620,7 @@ int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, con
   HIPC(hipMemcpyAsync(d_msgs, msgs32, 32 * n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * n, hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n, hipMemcpyHostToDevice, s));
-  if ((rc = run_verify_batch(n, d_pks, d_msgs, d_sigs, d_doms, d_v, ws, s))) return rc;
+  if ((rc = run_verify_batch(c, n, d_pks, d_msgs, d_sigs, d_doms, d_v, ws, s))) return rc;
   HIPC(hipMemcpyAsync(verdicts_out, d_v, n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;

@@ -753,16 +753,19 @@ BLS_INLINE fp12_g<E> fp12_cyclotomic_sqr_inl(const fp12_g<E>& f) {
   sq4(a0, b1, A0, A1);
   sq4(b0, a2, B0, B1);
   sq4(a1, b2, C0, C1);
+  // 3X - 2x = X + 2(X - x) and 3X + 2x = X + 2(X + x): three additions each
+  auto m3s2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_sub(X, x))); };
+  auto m3a2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_add(X, x))); };
   fp12_g<E> r;
   // A'
-  r.c0.c0 = fp2_sub(fp2_mul_small(A0, 3), fp2_dbl(a0));
-  r.c1.c1 = fp2_add(fp2_mul_small(A1, 3), fp2_dbl(b1));
+  r.c0.c0 = m3s2(A0, a0);
+  r.c1.c1 = m3a2(A1, b1);
   // B' = 3 z C^2 + 2 conj(B);  z (C0 + C1 z) = xi C1 + C0 z
-  r.c1.c0 = fp2_add(fp2_mul_small(fp2_mul_xi(C1), 3), fp2_dbl(b0));
-  r.c0.c2 = fp2_sub(fp2_mul_small(C0, 3), fp2_dbl(a2));
+  r.c1.c0 = m3a2(fp2_mul_xi(C1), b0);
+  r.c0.c2 = m3s2(C0, a2);
   // C'
-  r.c0.c1 = fp2_sub(fp2_mul_small(B0, 3), fp2_dbl(a1));
-  r.c1.c2 = fp2_add(fp2_mul_small(B1, 3), fp2_dbl(b2));
+  r.c0.c1 = m3s2(B0, a1);
+  r.c1.c2 = m3a2(B1, b2);
   return r;
 }
 
