@@ -741,31 +741,31 @@ BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E
 //   A' = 3A^2 - 2 conj(A),  B' = 3 z C^2 + 2 conj(B),  C' = 3 B^2 - 2 conj(C)
 template <class E>
 BLS_INLINE fp12_g<E> fp12_cyclotomic_sqr_inl(const fp12_g<E>& f) {
-  const E& a0 = f.c0.c0; const E& a1 = f.c0.c1; const E& a2 = f.c0.c2;
-  const E& b0 = f.c1.c0; const E& b1 = f.c1.c1; const E& b2 = f.c1.c2;
   auto sq4 = [](const E& x0, const E& x1, E& r0, E& r1) {
     const E t0 = fp2_sqr(x0);
     const E t1 = fp2_sqr(x1);
     r0 = fp2_add(t0, fp2_mul_xi(t1));
     r1 = fp2_sub(fp2_sqr(fp2_add(x0, x1)), fp2_add(t0, t1));
   };
-  E A0, A1, B0, B1, C0, C1;
-  sq4(a0, b1, A0, A1);
-  sq4(b0, a2, B0, B1);
-  sq4(a1, b2, C0, C1);
   // 3X - 2x = X + 2(X - x) and 3X + 2x = X + 2(X + x): three additions each
   auto m3s2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_sub(X, x))); };
   auto m3a2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_add(X, x))); };
+  // Each group's outputs are formed as soon as its squares exist, so few Fp2
+  // values stay live across the squaring calls (register pressure, not math).
   fp12_g<E> r;
-  // A'
-  r.c0.c0 = m3s2(A0, a0);
-  r.c1.c1 = m3a2(A1, b1);
-  // B' = 3 z C^2 + 2 conj(B);  z (C0 + C1 z) = xi C1 + C0 z
-  r.c1.c0 = m3a2(fp2_mul_xi(C1), b0);
-  r.c0.c2 = m3s2(C0, a2);
-  // C'
-  r.c0.c1 = m3s2(B0, a1);
-  r.c1.c2 = m3a2(B1, b2);
+  E X0, X1;
+  // A' = 3A^2 - 2 conj(A), A = a0 + b1 z
+  sq4(f.c0.c0, f.c1.c1, X0, X1);
+  r.c0.c0 = m3s2(X0, f.c0.c0);
+  r.c1.c1 = m3a2(X1, f.c1.c1);
+  // B' = 3 z C^2 + 2 conj(B), C = a1 + b2 z, B = b0 + a2 z;  z (C0 + C1 z) = xi C1 + C0 z
+  sq4(f.c0.c1, f.c1.c2, X0, X1);
+  r.c1.c0 = m3a2(fp2_mul_xi(X1), f.c1.c0);
+  r.c0.c2 = m3s2(X0, f.c0.c2);
+  // C' = 3B^2 - 2 conj(C)
+  sq4(f.c1.c0, f.c0.c2, X0, X1);
+  r.c0.c1 = m3s2(X0, f.c0.c1);
+  r.c1.c2 = m3a2(X1, f.c1.c2);
   return r;
 }
 

@@ -118,15 +118,20 @@ BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P) {
   return miller_loop_n<1>(&Q, &P);
 }
 
-// f^|x| in the cyclotomic subgroup, then conjugate for x < 0
-// One call per exponentiation: the 63 squarings are inlined so r stays in
-// registers across the loop (a call per squaring would pass r through scratch).
+// f^|x| in the cyclotomic subgroup, then conjugate for x < 0.
+// |x| = 0xd201000000010000 has bits 63, 62, 60, 57, 48, 16: after r = f the
+// squarings come in runs of 1, 2, 3, 9, 32 (each followed by r *= f) and a
+// final 16.  One call per exponentiation; the runs are tight loops of inlined
+// cyclotomic squarings, so r stays in registers (only the five products pass
+// it through memory).
+BLS_CONST int CYC_X_RUNS[6] = {1, 2, 3, 9, 32, 16};
+
 template <class E>
 BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   fp12_g<E> r = f;
-  for (int i = 62; i >= 0; --i) {
-    r = fp12_cyclotomic_sqr_inl(r);
-    if ((BLS_X_ABS >> i) & 1) r = fp12_mul(r, f);
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fp12_cyclotomic_sqr_inl(r);
+    if (s < 5) r = fp12_mul(r, f);
   }
   return fp12_conj(r);
 }
