@@ -99,6 +99,30 @@ def load_valu_peak():
         return None, None
 
 
+# profile key (bls381_profile_read) -> kernel symbol in rocprofv3 / PMC output
+PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2", "hash_to_g2": "k_hash_g2",
+                  "miller_loop_2": "k_miller_verify", "final_exp": "k_final_exp_verdict"}
+
+
+def load_pmc_traffic(prof_key, n):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC pass
+    (profiles/pmc_<tag>_counters.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc
+    runs of tools/prof_workload.py at the same n; FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM").
+    PMC counters cannot be read inside the timed run, so this is the last profiled build's figure."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_counters.json")), key=os.path.getmtime)
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            k = d["kernels"][PROFILE_KERNEL[prof_key]]
+            if int(k.get("waves", 0)) * 64 not in (n, 2 * n):   # lanes = n (G1) or 2n (lane-pair)
+                continue
+            return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+        except Exception:
+            continue
+    return None, None
+
+
 def count_fp_muls(pks, msgs, sigs, doms, k=8):
     """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build."""
     import build_native
@@ -388,9 +412,11 @@ def main():
     peak, peak_src = load_valu_peak()
     launch_macs = counts.get(dom_k, 0.0) * MACS_PER_FP_MUL * n
     achieved = launch_macs / (kern_ms[dom_k] * 1e-3) / 1e12
+    traffic, traffic_src = load_pmc_traffic(dom_k, n)
     roofline = {"bound": "valu-int32", "kernel": dom_k, "achieved": round(achieved, 3),
                 "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
-                "frac": round(achieved / peak, 4) if peak else None, "traffic": None,
+                "frac": round(achieved / peak, 4) if peak else None, "traffic": traffic,
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                 "macs_per_launch": launch_macs,
                 "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
                 "peak_source": peak_src}

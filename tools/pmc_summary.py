@@ -3,6 +3,7 @@
 Usage: python tools/pmc_summary.py gpurun_out/pmc_TAG [out.md]
 """
 import csv
+import json
 import glob
 import os
 import re
@@ -57,6 +58,15 @@ def main():
     print(out)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(out + "\n")
+        # machine-readable companion read by bench.py (roofline.traffic): HBM bytes per launch of each
+        # kernel, FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM" (gfx950 tallies 128-B reads at 64 B)
+        js = {k: {"hbm_bytes_per_launch": 2 * data[k].get("FETCH_SIZE", 0) * 1024 + data[k].get("WRITE_SIZE", 0) * 1024,
+                  "fetch_kb": data[k].get("FETCH_SIZE"), "write_kb": data[k].get("WRITE_SIZE"),
+                  "valu_insts": data[k].get("SQ_INSTS_VALU"), "waves": data[k].get("SQ_WAVES"),
+                  "wait_any_frac": data[k].get("SQ_WAIT_ANY", 0) / max(data[k].get("SQ_WAVE_CYCLES", 1), 1)}
+              for k in kernels}
+        json.dump({"source": os.path.basename(os.path.normpath(d)), "workload": "tools/prof_workload.py",
+                   "kernels": js}, open(os.path.splitext(sys.argv[2])[0] + ".json", "w"), indent=1)
 
 
 if __name__ == "__main__":
