@@ -225,6 +225,50 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
             "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world}
 
 
+def bench_registry_c3(native, L, args, pks, idx, offsets, d_ref_out, world, dist, dev, stream, t_u8):
+    """C3 committees aggregated from the device-resident pubkey registry: the
+    same 1024 x 128 members as validator indices into a registry of the 2^16 keys (the reference reads
+    state.validator_registry[i].pubkey, 0_beacon-chain.md:1025-1026).  Output bytes must equal the
+    decode-every-key path's."""
+    import torch
+    from bls381_amd.registry import PubkeyRegistry
+    n = len(pks) // 48
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reg = PubkeyRegistry(n)
+    ent = reg.add([pks[48 * i:48 * i + 48] for i in range(n)])
+    build_s = time.perf_counter() - t0
+    assert np.all(ent >= 0)
+    nc = len(offsets) - 1
+    ent_idx = ent[idx].astype(np.uint32)          # duplicate keys resolve to their first entry
+    d_idx = t_u8(ent_idx.tobytes())
+    d_out = torch.zeros(nc * 48, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nc, dtype=torch.int32, device=dev)
+    ws = torch.empty(L.bls381_registry_aggregate_workspace_size(nc, len(idx)), dtype=torch.uint8, device=dev)
+
+    def step():
+        native.check(L.bls381_registry_aggregate_indices_device(
+            reg._h, nc, offsets.ctypes.data_as(ctypes.c_void_p), len(idx), d_idx.data_ptr(), d_out.data_ptr(),
+            d_st.data_ptr(), ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    step()
+    torch.cuda.synchronize()
+    assert torch.equal(d_out, d_ref_out) and int(d_st.abs().sum().item()) == 0, "registry aggregation mismatch"
+    steps = max(args.steps, 3) * 4
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t = _max_time(time.perf_counter() - t0, world, dist, dev)
+    reg.close()
+    return {"workload": "C3 committees by validator index from a registry of %d decoded pubkeys" % n,
+            "committee_aggregations_per_s": nc * steps * world / t,
+            "pubkeys_aggregated_per_s": nc * (len(idx) // nc) * steps * world / t,
+            "ms_per_step": 1e3 * t / steps, "registry_build_ms": 1e3 * build_s,
+            "registry_build_keys_per_s": n / build_s}
+
+
 def bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist):
     """C4: 2^17 pubkeys/GPU -> one partial per GPU, RCCL all-gather, rank 0 sums."""
     import torch
@@ -393,6 +437,7 @@ def main():
                "committee_aggregations_per_s": nc * a_steps * world / at,
                "pubkeys_aggregated_per_s": nc * cs * a_steps * world / at,
                "ms_per_step": 1e3 * at / a_steps}
+        agg["registry"] = bench_registry_c3(native, L, args, pks, idx, offsets, d_out, world, dist, dev, stream, t_u8)
 
     sec = {}
     if not args.no_secondary:

@@ -86,11 +86,25 @@ def bls_verify_multiple(pubkeys, message_hashes, signature, domain):
     return _native.verify_multiple(b"".join(pks), b"".join(msgs), mlen, signature, dom8)
 
 
+# Optional device-resident pubkey registry (registry.PubkeyRegistry): when set,
+# bls_aggregate_pubkeys reads registered members' decoded points from HBM
+# instead of decompressing them.  Same bytes and errors either way.
+_pubkey_registry = None
+
+
+def use_pubkey_registry(registry) -> None:
+    """Route bls_aggregate_pubkeys through `registry` (None switches it off)."""
+    global _pubkey_registry
+    _pubkey_registry = registry
+
+
 @only_with_bls(alt_return=STUB_PUBKEY)
 def bls_aggregate_pubkeys(pubkeys):
     pks = [bytes(p) for p in pubkeys]
     if any(len(p) != 48 for p in pks):
         raise ValueError("pubkeys must be 48 bytes")
+    if _pubkey_registry is not None:
+        return _pubkey_registry.aggregate_pubkeys(pks)
     return _native.aggregate_pubkeys(b"".join(pks))
 
 

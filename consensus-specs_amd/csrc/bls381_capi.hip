@@ -269,7 +269,8 @@ size_t agg_ws_size(const AggPlan& p, int ncomp) {
 // runs the plan; returns device pointers to the final per-group Jacobian sums / bad flags
 template <class F>
 int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStream_t s,
-            const uint32_t** out_jac, const uint8_t** out_bad, size_t* used, size_t cap = SIZE_MAX) {
+            const uint32_t** out_jac, const uint8_t** out_bad, size_t* used, size_t cap = SIZE_MAX,
+            const agg_reg_src* reg = nullptr) {
   Bump b(ws, cap);
   const uint32_t* prev_jac = nullptr;
   const uint8_t* prev_bad = nullptr;
@@ -280,12 +281,18 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
     uint32_t* jac = b.take<uint32_t>(lv.size() * soa_jac<F>::NC * FP_LIMBS);
     uint8_t* bad = b.take<uint8_t>(lv.size());
     HIPC(hipMemcpyAsync(d_chunks, lv.data(), lv.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
-    if (l == 0) {
-      LAUNCH("agg_decode_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, true>), (size_t)lv.size(),
-             (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0, (const uint8_t*)nullptr, jac, bad);
+    const agg_reg_src none{nullptr, nullptr, nullptr, 0, 0};
+    if (l == 0 && reg) {
+      LAUNCH("agg_registry_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_REGISTRY>),
+             (size_t)lv.size(), (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0,
+             (const uint8_t*)nullptr, jac, bad, *reg);
+    } else if (l == 0) {
+      LAUNCH("agg_decode_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_BYTES>), (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0, (const uint8_t*)nullptr, jac, bad,
+             none);
     } else {
-      LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, false>), (size_t)lv.size(),
-             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad);
+      LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_JAC>), (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad, none);
     }
     prev_jac = jac;
     prev_bad = bad;
@@ -984,6 +991,213 @@ int bls381_hash_to_g2_pyecc_projective(size_t n, const uint8_t* msgs32, const ui
 } catch (const std::exception& e) {
   t_err = e.what();
   return BLS381_EARG;
+}
+
+// ---- pubkey registry
+struct bls381_registry {
+  int device = -1;
+  size_t cap = 0, size = 0;
+  uint32_t tmask = 0;
+  uint8_t* keys = nullptr;    // cap x 48 B
+  uint32_t* aff = nullptr;    // SoA affine, 2 x 14 words x cap
+  uint8_t* st = nullptr;      // cap entry statuses
+  uint32_t* table = nullptr;  // tmask + 1 slots
+  int32_t* tmp = nullptr;     // cap scratch entries (add / lookup results)
+  std::mutex mu;
+};
+
+static void registry_free(bls381_registry* r) {
+  if (!r) return;
+  (void)hipFree(r->keys); (void)hipFree(r->aff); (void)hipFree(r->st); (void)hipFree(r->table); (void)hipFree(r->tmp);
+  delete r;
+}
+
+int bls381_registry_create(size_t capacity, bls381_registry** out) {
+  if (!out || capacity == 0 || capacity > (size_t)INT32_MAX / 2) return BLS381_EARG;
+  *out = nullptr;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  auto* r = new bls381_registry();
+  r->device = c->device;
+  r->cap = capacity;
+  size_t t = 1;
+  while (t < 2 * capacity) t <<= 1;
+  r->tmask = (uint32_t)(t - 1);
+  if (hipMalloc(&r->keys, 48 * capacity) != hipSuccess || hipMalloc(&r->aff, 2 * FPW * capacity) != hipSuccess ||
+      hipMalloc(&r->st, capacity) != hipSuccess || hipMalloc(&r->table, 4 * t) != hipSuccess ||
+      hipMalloc(&r->tmp, 4 * capacity) != hipSuccess) {
+    registry_free(r);
+    t_err = "registry allocation failed";
+    return BLS381_EHIP;
+  }
+  if (hipMemsetAsync(r->table, 0xFF, 4 * t, c->stream) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+    registry_free(r);
+    t_err = "registry init failed";
+    return BLS381_EHIP;
+  }
+  *out = r;
+  return 0;
+}
+
+void bls381_registry_destroy(bls381_registry* reg) {
+  if (!reg) return;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (c) (void)hipStreamSynchronize(c->stream);
+  registry_free(reg);
+}
+
+size_t bls381_registry_size(const bls381_registry* reg) { return reg ? reg->size : 0; }
+
+static Ctx* registry_ctx(bls381_registry* reg, int* rc) {
+  Ctx* c = get_ctx(rc);
+  if (c && c->device != reg->device) { t_err = "registry belongs to another device"; *rc = BLS381_EARG; return nullptr; }
+  return c;
+}
+
+int bls381_registry_add(bls381_registry* reg, size_t n, const uint8_t* pks48, int32_t* entry_out) {
+  if (!reg || (n && !pks48)) return BLS381_EARG;
+  if (n == 0) return 0;
+  int rc = 0;
+  Ctx* c = registry_ctx(reg, &rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lr(reg->mu);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (reg->size + n > reg->cap) { t_err = "registry capacity exceeded"; return BLS381_EARG; }
+  hipStream_t s = c->stream;
+  const size_t first = reg->size;
+  HIPC(hipMemcpyAsync(reg->keys + 48 * first, pks48, 48 * n, hipMemcpyHostToDevice, s));
+  LAUNCH("registry_decode", s, dim3(grid_for(n)), dim3(KBLOCK), k_reg_decode, first, n, reg->cap,
+         (const uint8_t*)reg->keys, reg->aff, reg->st);
+  LAUNCH("registry_insert", s, dim3(grid_for(n)), dim3(KBLOCK), k_reg_insert, first, n, (const uint8_t*)reg->keys,
+         (const uint8_t*)reg->st, reg->table, reg->tmask);
+  LAUNCH("registry_lookup", s, dim3(grid_for(n)), dim3(KBLOCK), k_reg_lookup, n,
+         (const uint8_t*)(reg->keys + 48 * first), (const uint8_t*)reg->keys, (const uint32_t*)reg->table, reg->tmask,
+         reg->tmp);
+  std::vector<int32_t> res(n);
+  HIPC(hipMemcpyAsync(res.data(), reg->tmp, 4 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  reg->size += n;
+  int nbad = 0;
+  for (size_t i = 0; i < n; ++i) nbad += res[i] < 0;
+  if (entry_out) std::memcpy(entry_out, res.data(), 4 * n);
+  return nbad;
+}
+
+int bls381_registry_lookup(bls381_registry* reg, size_t n, const uint8_t* pks48, int32_t* entry_out) try {
+  if (!reg || (n && (!pks48 || !entry_out))) return BLS381_EARG;
+  if (n == 0) return 0;
+  int rc = 0;
+  Ctx* c = registry_ctx(reg, &rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lr(reg->mu);
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, align256(48 * n) + align256(4 * n) + 1024))) return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_q = b.take<uint8_t>(48 * n);
+  int32_t* d_e = b.take<int32_t>(n);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_q, pks48, 48 * n, hipMemcpyHostToDevice, s));
+  LAUNCH("registry_lookup", s, dim3(grid_for(n)), dim3(KBLOCK), k_reg_lookup, n, (const uint8_t*)d_q,
+         (const uint8_t*)reg->keys, (const uint32_t*)reg->table, reg->tmask, d_e);
+  HIPC(hipMemcpyAsync(entry_out, d_e, 4 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  int hits = 0;
+  for (size_t i = 0; i < n; ++i) hits += entry_out[i] >= 0;
+  return hits;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+// groups of registry entries (d_entry, device) or of compressed keys looked up first (d_pks); one pass of the
+// chunked tree, then compression.  Returns once queued on s.
+static int registry_agg_impl(Ctx* c, bls381_registry* reg, size_t ng, const uint32_t* offsets, size_t n_in,
+                             const int32_t* d_entry, const uint8_t* d_pks, uint8_t* d_out, int32_t* d_status,
+                             void* ws, size_t ws_cap, hipStream_t s) {
+  Bump b(ws, ws_cap);
+  if (!d_entry) {
+    int32_t* e = b.take<int32_t>(n_in + 1);
+    LAUNCH("registry_lookup", s, dim3(grid_for(n_in)), dim3(KBLOCK), k_reg_lookup, n_in, d_pks,
+           (const uint8_t*)reg->keys, (const uint32_t*)reg->table, reg->tmask, e);
+    d_entry = e;
+  }
+  auto hold = std::make_shared<AggPlan>(plan_agg(ng, offsets));
+  const agg_reg_src src{d_entry, reg->aff, reg->st, reg->cap, reg->size};
+  const uint32_t* jac;
+  const uint8_t* bad;
+  size_t used = 0;
+  int rc = run_agg<fp_t>(*hold, ng, d_pks, b.base + align256(b.off), s, &jac, &bad, &used, b.left() - 256, &src);
+  if (rc) return rc;
+  LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
+  return keep_until_done(c, s, hold);
+}
+
+size_t bls381_registry_aggregate_workspace_size(size_t n_groups, size_t n_in) {
+  return align256(4 * (n_in + 1)) + bls381_aggregate_pubkeys_batch_workspace_size(n_groups, n_in) + 4096;
+}
+
+int bls381_registry_aggregate_indices_device(bls381_registry* reg, size_t n_groups, const uint32_t* h_offsets,
+                                             size_t n_idx, const uint32_t* d_indices, uint8_t* d_out48,
+                                             int32_t* d_status, void* d_workspace, void* stream) try {
+  if (!reg || !h_offsets || !d_out48 || !d_status || !d_workspace || (n_idx && !d_indices)) return BLS381_EARG;
+  if (n_groups == 0) return 0;
+  if (h_offsets[n_groups] != n_idx) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = registry_ctx(reg, &rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lr(reg->mu);
+  return registry_agg_impl(c, reg, n_groups, h_offsets, n_idx, (const int32_t*)d_indices, nullptr, d_out48, d_status,
+                           d_workspace, bls381_registry_aggregate_workspace_size(n_groups, n_idx), (hipStream_t)stream);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+static int registry_agg_host(bls381_registry* reg, size_t ng, const uint32_t* offsets, const uint32_t* indices,
+                             const uint8_t* pks, uint8_t* out48, int32_t* status) try {
+  int rc = 0;
+  Ctx* c = registry_ctx(reg, &rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lr(reg->mu);
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t n_in = offsets[ng];
+  const size_t wsb = bls381_registry_aggregate_workspace_size(ng, n_in);
+  const size_t need = align256(n_in * (indices ? 4 : 48) + 1) + align256(48 * ng) + align256(4 * ng) + wsb + 1024;
+  if ((rc = ensure_ws(c, need))) return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_in = b.take<uint8_t>(n_in * (indices ? 4 : 48) + 1);
+  uint8_t* d_out = b.take<uint8_t>(48 * ng);
+  int32_t* d_st = b.take<int32_t>(ng);
+  uint8_t* d_ws = b.take<uint8_t>(wsb);
+  hipStream_t s = c->stream;
+  if (n_in) HIPC(hipMemcpyAsync(d_in, indices ? (const void*)indices : (const void*)pks, n_in * (indices ? 4 : 48),
+                                hipMemcpyHostToDevice, s));
+  if ((rc = registry_agg_impl(c, reg, ng, offsets, n_in, indices ? (const int32_t*)d_in : nullptr,
+                              indices ? nullptr : d_in, d_out, d_st, d_ws, wsb, s)))
+    return rc;
+  HIPC(hipMemcpyAsync(out48, d_out, 48 * ng, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(status, d_st, 4 * ng, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_registry_aggregate_indices(bls381_registry* reg, size_t n_groups, const uint32_t* offsets,
+                                      const uint32_t* indices, uint8_t* out48, int32_t* status) {
+  if (!reg || !offsets || !out48 || !status || (offsets[n_groups] && !indices)) return BLS381_EARG;
+  if (n_groups == 0) return 0;
+  return registry_agg_host(reg, n_groups, offsets, indices, nullptr, out48, status);
+}
+
+int bls381_registry_aggregate_pubkeys_batch(bls381_registry* reg, size_t n_groups, const uint32_t* offsets,
+                                            const uint8_t* pks, uint8_t* out48, int32_t* status) {
+  if (!reg || !offsets || !out48 || !status || (offsets[n_groups] && !pks)) return BLS381_EARG;
+  if (n_groups == 0) return 0;
+  return registry_agg_host(reg, n_groups, offsets, nullptr, pks, out48, status);
 }
 
 }  // extern "C"

@@ -209,12 +209,33 @@ template <> struct pt_traits<fp2p_t> {
   __device__ static int decode(aff_t<fp2p_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
 };
 
-template <class F, bool LEVEL1>
+template <class F> __device__ aff_t<F> reg_ld_aff(const uint32_t* aff, size_t cap, size_t r);
+template <> __device__ __forceinline__ aff_t<fp_t> reg_ld_aff<fp_t>(const uint32_t* aff, size_t cap, size_t r) {
+  return soa_ld_g1(aff, cap, r);
+}
+template <> __device__ __forceinline__ aff_t<fp2p_t> reg_ld_aff<fp2p_t>(const uint32_t*, size_t, size_t) {
+  __builtin_trap();   // the registry holds G1 pubkeys only; never instantiated with entries
+}
+
+// Inputs of a level-1 chunk sum: compressed bytes, or (AGG_REGISTRY, G1 only) a
+// registry entry per input -- entry >= 0 reads the registry's decoded point,
+// entry < 0 decodes the input's own bytes (a cache miss).
+enum : int { AGG_BYTES = 0, AGG_JAC = 1, AGG_REGISTRY = 2 };
+struct agg_reg_src {
+  const int32_t* entry;   // per input: registry entry or -1
+  const uint32_t* aff;    // registry SoA affine points (stride cap)
+  const uint8_t* st;      // registry entry status: ST_OK / ST_INF / ST_BAD
+  size_t cap;             // SoA stride
+  size_t size;            // entries in use: an entry >= size is an error (BAD), never read
+};
+
+template <class F, int MODE>
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                       const uint8_t* __restrict__ in_bytes,
                                                       const uint32_t* __restrict__ in_jac, size_t n_in,
                                                       const uint8_t* __restrict__ in_bad,
-                                                      uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad) {
+                                                      uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad,
+                                                      agg_reg_src reg) {
   constexpr int LPI = lanes_per<F>::N;
   constexpr int NW = sizeof(jac_t<F>) / 4;   // words per lane
   __shared__ uint32_t lds[KBLOCK * NW];
@@ -228,15 +249,25 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t 
   bool bad = false;
   const uint32_t slot = threadIdx.x / LPI;
   for (uint32_t e = ch.begin + slot; e < ch.end; e += KBLOCK / LPI) {
-    if (LEVEL1) {
-      aff_t<F> a;
-      const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
-      if (s == PT_BAD) bad = true;
-      else if (s == PT_OK) acc = jac_add_aff(acc, a);
-    } else {
+    if (MODE == AGG_JAC) {
       if (in_bad[e]) bad = true;
       acc = jac_add(acc, soa_jac<F>::ld(in_jac, n_in, e));
+      continue;
     }
+    if (MODE == AGG_REGISTRY) {
+      const int32_t r = reg.entry ? reg.entry[e] : -1;
+      if ((r >= 0 && (size_t)r >= reg.size) || (r < 0 && !in_bytes)) { bad = true; continue; }
+      if (r >= 0) {
+        const uint8_t rs = reg.st[r];
+        if (rs == ST_BAD) bad = true;
+        else if (rs == ST_OK) acc = jac_add_aff(acc, reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r));
+        continue;
+      }
+    }
+    aff_t<F> a;
+    const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
+    if (s == PT_BAD) bad = true;
+    else if (s == PT_OK) acc = jac_add_aff(acc, a);
   }
   if (bad) bad_any = 1;
   // tree reduction through LDS (lane-major words: conflict-free stride-1 access);
@@ -293,6 +324,83 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g1_affine(size
   if (!g1_in_subgroup(a)) { st[g] = ST_BAD; return; }
   soa_st_g1(out_aff, ng, g, a);
   st[g] = ST_OK;
+}
+
+// -------------------------------------------------------- pubkey registry --
+// Device-resident registry of decoded pubkeys: entry j
+// holds the 48-byte key, its status and its affine point (SoA, stride cap); an
+// open-addressing table (u32 entry per slot, REG_EMPTY when free, linear
+// probing, power-of-two size) maps key bytes to entries.
+constexpr uint32_t REG_EMPTY = 0xFFFFFFFFu;
+
+// 48 key bytes -> 32-bit hash (all 12 words mixed; the x bytes are uniform)
+__device__ __forceinline__ uint32_t reg_hash(const uint8_t* k) {
+  uint32_t h = 0x9E3779B9u;
+  for (int w = 0; w < 12; ++w) {
+    const uint32_t v = (uint32_t)k[4 * w] | ((uint32_t)k[4 * w + 1] << 8) | ((uint32_t)k[4 * w + 2] << 16) |
+                       ((uint32_t)k[4 * w + 3] << 24);
+    h = (h ^ v) * 0x85EBCA6Bu;
+    h ^= h >> 15;
+  }
+  return h;
+}
+__device__ __forceinline__ bool reg_key_eq(const uint8_t* a, const uint8_t* b) {
+  uint32_t d = 0;
+  for (int i = 0; i < 48; ++i) d |= (uint32_t)(a[i] ^ b[i]);
+  return d == 0;
+}
+
+// decode keys [first, first + n) in place (status + affine point)
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_reg_decode(size_t first, size_t n, size_t cap,
+                                                      const uint8_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ aff, uint8_t* __restrict__ st) {
+  const size_t t = item_index<1>();
+  if (t >= n) return;
+  const size_t j = first + t;
+  aff_t<fp_t> a;
+  const int s = g1_decompress(a, keys + 48 * j);
+  if (s == PT_OK) soa_st_g1(aff, cap, j, a);
+  st[j] = s == PT_OK ? ST_OK : (s == PT_INF ? ST_INF : ST_BAD);
+}
+
+// insert entries [first, first + n) that decoded.  Equal keys share one slot,
+// which ends up holding the smallest of their entries (atomicMin), whatever
+// the order the lanes run in; the caller then resolves each key with
+// k_reg_lookup once the table has settled.
+__global__ void __launch_bounds__(KBLOCK) k_reg_insert(size_t first, size_t n, const uint8_t* __restrict__ keys,
+                                                       const uint8_t* __restrict__ st, uint32_t* table, uint32_t mask) {
+  const size_t t = item_index<1>();
+  if (t >= n) return;
+  const uint32_t j = (uint32_t)(first + t);
+  if (st[j] == ST_BAD) return;
+  const uint8_t* k = keys + 48 * (size_t)j;
+  uint32_t slot = reg_hash(k) & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe, slot = (slot + 1) & mask) {
+    uint32_t cur = __atomic_load_n(&table[slot], __ATOMIC_RELAXED);
+    if (cur == REG_EMPTY) {
+      cur = atomicCAS(&table[slot], REG_EMPTY, j);
+      if (cur == REG_EMPTY) return;
+    }
+    if (reg_key_eq(keys + 48 * (size_t)cur, k)) { atomicMin(&table[slot], j); return; }
+  }
+}
+
+// content-addressed lookup of n compressed keys: entry or -1 (not registered)
+__global__ void __launch_bounds__(KBLOCK) k_reg_lookup(size_t n, const uint8_t* __restrict__ q,
+                                                       const uint8_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ table, uint32_t mask,
+                                                       int32_t* __restrict__ entry) {
+  const size_t t = item_index<1>();
+  if (t >= n) return;
+  const uint8_t* k = q + 48 * t;
+  uint32_t slot = reg_hash(k) & mask;
+  int32_t r = -1;
+  for (uint32_t probe = 0; probe <= mask; ++probe, slot = (slot + 1) & mask) {
+    const uint32_t cur = table[slot];
+    if (cur == REG_EMPTY) break;
+    if (reg_key_eq(keys + 48 * (size_t)cur, k)) { r = (int32_t)cur; break; }
+  }
+  entry[t] = r;
 }
 
 // ------------------------------------------------------- sign / privtopub --

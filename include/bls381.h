@@ -138,6 +138,43 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
 /* Multiply k partial products and run one final exponentiation: 1 / 0. */
 int bls381_final_verify(size_t k, const uint8_t* parts576);
 
+/* ---- device-resident pubkey registry ---------------- */
+/* Decoded validator pubkeys kept in HBM, so committee aggregation reads each
+ * member's point instead of decompressing it (the per-key Fp square root that
+ * dominates bls_aggregate_pubkeys).  The reference indexes pubkeys through
+ * state.validator_registry (specs/core/0_beacon-chain.md:1025-1026, the
+ * get_attesting_indices -> bls_aggregate_pubkeys call of
+ * validate_indexed_attestation); aggregation over the registry returns the same
+ * bytes as bls_aggregate_pubkeys over the members' encodings (bls.py:34-36).
+ * Entries are appended in order: entry e is the e-th key ever added (the
+ * validator index when keys are added in registry order).  One registry belongs
+ * to the device current at creation. */
+typedef struct bls381_registry bls381_registry;
+int bls381_registry_create(size_t capacity, bls381_registry** out);
+void bls381_registry_destroy(bls381_registry* reg);
+size_t bls381_registry_size(const bls381_registry* reg);
+/* Append n keys as entries [size, size+n).  entry_out[i] (may be NULL) is the
+ * entry that now holds key i's bytes (its own, or an earlier duplicate's), or
+ * -1 when key i does not decode.  Returns the number of keys that do not decode. */
+int bls381_registry_add(bls381_registry* reg, size_t n, const uint8_t* pks48, int32_t* entry_out);
+/* Content-addressed lookup: entry_out[i] = entry holding key i's bytes, or -1.
+ * Returns the number of hits. */
+int bls381_registry_lookup(bls381_registry* reg, size_t n, const uint8_t* pks48, int32_t* entry_out);
+/* Group g = entries indices[offsets[g] .. offsets[g+1]); status as for
+ * bls381_aggregate_pubkeys_batch (an undecodable or out-of-range entry makes
+ * its group BLS381_EINVAL_POINT). */
+int bls381_registry_aggregate_indices(bls381_registry* reg, size_t n_groups, const uint32_t* offsets,
+                                      const uint32_t* indices, uint8_t* out48, int32_t* status);
+/* Same contract as bls381_aggregate_pubkeys_batch: members found in the
+ * registry are read from it, the others are decoded from their bytes. */
+int bls381_registry_aggregate_pubkeys_batch(bls381_registry* reg, size_t n_groups, const uint32_t* offsets,
+                                            const uint8_t* pks, uint8_t* out48, int32_t* status);
+size_t bls381_registry_aggregate_workspace_size(size_t n_groups, size_t n_idx);
+/* Device-pointer form of bls381_registry_aggregate_indices (h_offsets on the host). */
+int bls381_registry_aggregate_indices_device(bls381_registry* reg, size_t n_groups, const uint32_t* h_offsets,
+                                             size_t n_idx, const uint32_t* d_indices, uint8_t* d_out48,
+                                             int32_t* d_status, void* d_workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

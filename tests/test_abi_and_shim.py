@@ -92,3 +92,10 @@ def test_keyword_names_match_reference():
         fn = getattr(bls, name)
         inner = next(c.cell_contents for c in fn.__closure__ if callable(c.cell_contents))
         assert list(inspect.signature(inner).parameters) == params, name
+
+
+def test_registry_shim_hook_is_opt_in():
+    from bls381_amd import bls
+    assert bls._pubkey_registry is None
+    bls.use_pubkey_registry(None)
+    assert bls._pubkey_registry is None

@@ -431,3 +431,64 @@ def test_device_entry_points_order_on_torch_default_stream(native):
     native.check(L.bls381_verify_batch_device(4, *[x.data_ptr() for x in keep], d_v.data_ptr(),
                                               vws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
     assert d_v.cpu().tolist() == [1, 1, 0, 1]
+
+
+# ------------------------------------------ pubkey registry (§8(f) rank 1)
+def test_registry_matches_aggregate_pubkeys(native, golden):
+    """Registry aggregation (by index and by content lookup) == bls_aggregate_pubkeys bytes."""
+    from bls381_amd import bls
+    from bls381_amd.registry import PubkeyRegistry
+    _, gb = golden
+    inf = bytes([0xC0]) + b"\x00" * 47
+    keys = [O.privtopub(k) for k in range(1, 201)] + [inf]
+    bad = [bytes.fromhex(h) for h in gb["invalid_g1"]]
+    reg = PubkeyRegistry(1024)
+    ent = reg.add(keys + bad + keys[:3])            # bad keys -> -1, duplicates -> earlier entry
+    assert list(ent[:201]) == list(range(201))
+    assert all(e == -1 for e in ent[201:201 + len(bad)])
+    assert list(ent[201 + len(bad):]) == [0, 1, 2]
+    assert len(reg) == 201 + len(bad) + 3
+    assert list(reg.lookup([keys[7], keys[200], O.privtopub(999), bad[0]])) == [7, 200, -1, -1]
+    rng = random.Random(0xB15_0006)
+    groups = [rng.sample(range(201), 128) for _ in range(6)] + [[], [200], [3, 3, 3], list(range(201))]
+    got = reg.aggregate_indices(groups)
+    for g, out in zip(groups, got):
+        assert out == O.aggregate_pubkeys([keys[i] for i in g])
+    # content-addressed: registered, unregistered and infinity members mixed
+    extra = [O.privtopub(k) for k in range(1000, 1010)]
+    byte_groups = [[keys[i] for i in groups[0]] + extra, extra, [keys[5], inf], []]
+    got = reg.aggregate_pubkeys_batch(byte_groups)
+    for g, out in zip(byte_groups, got):
+        assert out == O.aggregate_pubkeys(g)
+    # the bls shim routed through the registry: same bytes, same errors
+    bls.use_pubkey_registry(reg)
+    try:
+        assert bls.bls_aggregate_pubkeys(byte_groups[0]) == O.aggregate_pubkeys(byte_groups[0])
+        for b in bad:
+            with pytest.raises(ValueError):
+                bls.bls_aggregate_pubkeys([keys[0], b])
+        assert bls.bls_aggregate_pubkeys([]) == inf
+    finally:
+        bls.use_pubkey_registry(None)
+    # a bad or out-of-range entry fails its group only
+    with pytest.raises(ValueError):
+        reg.aggregate_indices([[0, 201]])            # entry 201 holds an undecodable key
+    with pytest.raises(ValueError):
+        reg.aggregate_indices([[0, len(reg)]])       # past the end: never read
+    reg.close()
+
+
+def test_registry_large_multilevel(native):
+    """3000-member group through the registry (multi-level tree): sum [k]G = [sum k]G."""
+    from bls381_amd.registry import PubkeyRegistry
+    keys = [O.privtopub(k) for k in range(1, 41)]
+    reg = PubkeyRegistry(64)
+    reg.add(keys)
+    n = 3000
+    idx = [i % 40 for i in range(n)]
+    out = reg.aggregate_indices([idx, idx[:513]])
+    assert out[0] == O.privtopub(sum(i + 1 for i in idx))
+    assert out[1] == O.privtopub(sum(i + 1 for i in idx[:513]))
+    with pytest.raises(ValueError):
+        reg.add([keys[0]] * 100)                     # capacity 64 exceeded
+    reg.close()
