@@ -492,3 +492,15 @@ def test_registry_large_multilevel(native):
     with pytest.raises(ValueError):
         reg.add([keys[0]] * 100)                     # capacity 64 exceeded
     reg.close()
+
+
+# ---------------------------------------- YAML `bls` suites (§8(f) rank 4)
+def test_yaml_vectors_generate_and_run(native, golden, tmp_path):
+    """The engine regenerates all 94 generator cases bit-exact, and the runner passes them."""
+    from bls381_amd import bls, vector_runner as V
+    vec, _ = golden
+    cases = V.generate_cases(bls)
+    assert cases == vec
+    V.write_suites(str(tmp_path), cases)
+    res = V.run(str(tmp_path), bls)
+    assert sum(ok for ok, _ in res.values()) == 94 and not any(f for _, f in res.values())
