@@ -225,6 +225,47 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
             "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world}
 
 
+def bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8):
+    """C2 end to end from serialized DepositData: signing_root(deposit.data) on the
+    device feeding the verify pipeline (process_deposit, 0_beacon-chain.md:1755-1758), same keys as C2."""
+    import torch
+    from bls381_amd import ssz
+    n = len(pks) // 48
+    rng = np.random.default_rng(0xB15_0009)
+    wc = rng.bytes(32 * n)
+    amt = (32 * 10 ** 9 + np.arange(n, dtype=np.uint64)).astype("<u8").tobytes()
+    items = [pks[48 * i:48 * i + 48] + wc[32 * i:32 * i + 32] + amt[8 * i:8 * i + 8] + b"\x00" * 96 for i in range(n)]
+    roots = b"".join(ssz.signing_root_batch(ssz.DepositData, items))
+    sks = b"".join(k.to_bytes(32, "big") for k in sk_ints)
+    doms = DOMAIN_DEPOSIT.to_bytes(8, "big") * n
+    sigs = native.sign_batch(roots, sks, doms)
+    blob = bytearray(b"".join(items[i][:88] + sigs[96 * i:96 * i + 96] for i in range(n)))
+    expected = np.ones(n, dtype=bool)
+    for i in range(5, n, 16):              # 1/16 tampered: amount changed after signing
+        blob[184 * i + 80] ^= 0x01
+        expected[i] = False
+    d_dd, d_dom = t_u8(bytes(blob)), t_u8(doms)
+    d_ver = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.bls381_verify_deposits_workspace_size(n), dtype=torch.uint8, device=dev)
+
+    def step():
+        native.check(L.bls381_verify_deposits_device(n, d_dd.data_ptr(), d_dom.data_ptr(), d_ver.data_ptr(),
+                                                     ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    step()
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ver.cpu().numpy().astype(bool), expected), "deposit verdict mismatch"
+    steps = max(args.steps, 3)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t = _max_time(time.perf_counter() - t0, world, dist, dev)
+    return {"workload": "C2 from %d serialized DepositData per GPU: device signing_root + bls_verify" % n,
+            "deposits_per_s": n * steps * world / t, "ms_per_step": 1e3 * t / steps, "n_gpus": world}
+
+
 def bench_registry_c3(native, L, args, pks, idx, offsets, d_ref_out, world, dist, dev, stream, t_u8):
     """C3 committees aggregated from the device-resident pubkey registry: the
     same 1024 x 128 members as validator indices into a registry of the 2^16 keys (the reference reads
@@ -441,6 +482,7 @@ def main():
 
     sec = {}
     if not args.no_secondary:
+        sec["c2_deposits"] = bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8)
         sec["c3_epoch"] = bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist)
         sec["c4_aggregate"] = bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist)
         sec["c5_multi_pairing"] = bench_c5(native, args, world, rank, dist, dev)

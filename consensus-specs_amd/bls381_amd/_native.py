@@ -52,6 +52,13 @@ _SIGS = {
     "bls381_miller_partial": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int,
                                              _u8p, _u8p]),
     "bls381_final_verify": (ctypes.c_int, [ctypes.c_size_t, _u8p]),
+    "bls381_ssz_root_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, ctypes.c_uint32, _u8p]),
+    "bls381_ssz_root_workspace_size": (ctypes.c_size_t, []),
+    "bls381_ssz_root_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, ctypes.c_size_t, _u8p,
+                                                    ctypes.c_uint32, _u8p, _u8p, _u8p]),
+    "bls381_verify_deposits": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p]),
+    "bls381_verify_deposits_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t]),
+    "bls381_verify_deposits_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p]),
     "bls381_registry_create": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     "bls381_registry_destroy": (None, [ctypes.c_void_p]),
     "bls381_registry_size": (ctypes.c_size_t, [ctypes.c_void_p]),

@@ -1200,4 +1200,146 @@ int bls381_registry_aggregate_pubkeys_batch(bls381_registry* reg, size_t n_group
   return registry_agg_host(reg, n_groups, offsets, nullptr, pks, out48, status);
 }
 
+// ---- SSZ roots and the deposit pipeline
+size_t bls381_ssz_root_workspace_size(void) { return align256(4 * SSZ_PROG_MAX) + 256; }
+
+static int ssz_root_impl(size_t n, const uint8_t* d_items, size_t stride, const uint32_t* h_prog, uint32_t plen,
+                         uint8_t* d_roots, Bump& b, hipStream_t s, Ctx* c) {
+  uint32_t* d_prog = b.take<uint32_t>(SSZ_PROG_MAX);
+  int32_t* d_err = b.take<int32_t>(1);
+  auto prog = std::make_shared<std::vector<uint32_t>>(h_prog, h_prog + plen);
+  HIPC(hipMemcpyAsync(d_prog, prog->data(), 4 * plen, hipMemcpyHostToDevice, s));
+  HIPC(hipMemsetAsync(d_err, 0, 4, s));
+  LAUNCH("ssz_root", s, dim3(grid_for(n)), dim3(KBLOCK), k_ssz_root, n, d_items, stride, (const uint32_t*)d_prog,
+         plen, d_roots, d_err);
+  return keep_until_done(c, s, prog);
+}
+
+// host check of a program: balanced stack, chunk reads inside the item, sizes in bounds (the kernel
+// re-checks the stack; reads past the item are what this rules out)
+static bool ssz_prog_ok(const uint32_t* prog, uint32_t plen, size_t item_size) {
+  if (!prog || plen == 0 || plen > SSZ_PROG_MAX) return false;
+  int sp = 0, peak = 0;
+  for (uint32_t pc = 0; pc < plen;) {
+    if (prog[pc] == SSZ_CHUNK && pc + 2 < plen) {
+      if (prog[pc + 2] > 32 || (size_t)prog[pc + 1] + prog[pc + 2] > item_size) return false;
+      ++sp; pc += 3;
+    } else if (prog[pc] == SSZ_MERKLE && pc + 1 < plen) {
+      const uint32_t k = prog[pc + 1];
+      if (k == 0 || (int)k > sp) return false;
+      uint32_t p = 1;
+      while (p < k) p <<= 1;
+      if (sp - (int)k + (int)p > peak) peak = sp - (int)k + (int)p;
+      sp = sp - (int)k + 1; pc += 2;
+    } else {
+      return false;
+    }
+    if (sp > peak) peak = sp;
+  }
+  return sp == 1 && peak <= SSZ_STACK;
+}
+
+int bls381_ssz_root_batch_device(size_t n, const uint8_t* d_items, size_t stride, size_t item_size,
+                                 const uint32_t* h_prog, uint32_t prog_len, uint8_t* d_roots32, void* d_workspace,
+                                 void* stream) try {
+  if (n == 0) return 0;
+  if (!d_items || !d_roots32 || !d_workspace || stride < item_size || !ssz_prog_ok(h_prog, prog_len, item_size))
+    return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  Bump b(d_workspace, bls381_ssz_root_workspace_size());
+  return ssz_root_impl(n, d_items, stride, h_prog, prog_len, d_roots32, b, (hipStream_t)stream, c);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_ssz_root_batch(size_t n, const uint8_t* items, size_t item_size, const uint32_t* prog, uint32_t prog_len,
+                          uint8_t* roots32) try {
+  if (n == 0) return 0;
+  if (!items || !roots32 || item_size == 0 || !ssz_prog_ok(prog, prog_len, item_size)) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  if ((rc = ensure_ws(c, align256(n * item_size) + align256(32 * n) + bls381_ssz_root_workspace_size() + 1024)))
+    return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_items = b.take<uint8_t>(n * item_size);
+  uint8_t* d_roots = b.take<uint8_t>(32 * n);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_items, items, n * item_size, hipMemcpyHostToDevice, s));
+  if ((rc = ssz_root_impl(n, d_items, item_size, prog, prog_len, d_roots, b, s, c))) return rc;
+  HIPC(hipMemcpyAsync(roots32, d_roots, 32 * n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+// signing_root(DepositData) (0_beacon-chain.md:394-403; ssz_impl.py:158-163): pubkey Bytes48 (2 chunks),
+// withdrawal_credentials Bytes32, amount uint64; the signature field is left out
+static const uint32_t DEPOSIT_SIGNING_PROG[] = {SSZ_CHUNK, 0, 32, SSZ_CHUNK, 32, 16, SSZ_MERKLE, 2,
+                                                SSZ_CHUNK, 48, 32, SSZ_CHUNK, 80, 8, SSZ_MERKLE, 3};
+constexpr size_t DEPOSIT_DATA_BYTES = 48 + 32 + 8 + 96;
+
+size_t bls381_verify_deposits_workspace_size(size_t n) {
+  return align256(48 * n) + align256(96 * n) + align256(32 * n) + bls381_ssz_root_workspace_size() +
+         verify_ws_size(n) + 2048;
+}
+
+int bls381_verify_deposits_device(size_t n, const uint8_t* d_deposit_data, const uint8_t* d_dom8s,
+                                  uint8_t* d_verdicts, void* d_workspace, void* stream) try {
+  if (n == 0) return 0;
+  if (!d_deposit_data || !d_dom8s || !d_verdicts || !d_workspace) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  Bump b(d_workspace, bls381_verify_deposits_workspace_size(n));
+  uint8_t* pks = b.take<uint8_t>(48 * n);
+  uint8_t* sigs = b.take<uint8_t>(96 * n);
+  uint8_t* roots = b.take<uint8_t>(32 * n);
+  LAUNCH("gather_pubkeys", s, dim3(grid_for(48 * n)), dim3(KBLOCK), k_gather_field, n, d_deposit_data,
+         DEPOSIT_DATA_BYTES, 0u, 48u, pks);
+  LAUNCH("gather_signatures", s, dim3(grid_for(96 * n)), dim3(KBLOCK), k_gather_field, n, d_deposit_data,
+         DEPOSIT_DATA_BYTES, 88u, 96u, sigs);
+  if ((rc = ssz_root_impl(n, d_deposit_data, DEPOSIT_DATA_BYTES, DEPOSIT_SIGNING_PROG,
+                          (uint32_t)(sizeof(DEPOSIT_SIGNING_PROG) / 4), roots, b, s, c)))
+    return rc;
+  void* vws = b.take<uint8_t>(verify_ws_size(n));
+  return run_verify_batch(c, n, pks, roots, sigs, d_dom8s, d_verdicts, vws, s);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_verify_deposits(size_t n, const uint8_t* deposit_data, const uint8_t* dom8s, uint8_t* verdicts) try {
+  if (n == 0) return 0;
+  if (!deposit_data || !dom8s || !verdicts) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t wsb = bls381_verify_deposits_workspace_size(n);
+  if ((rc = ensure_ws(c, align256(DEPOSIT_DATA_BYTES * n) + align256(8 * n) + align256(n) + wsb + 1024))) return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_dd = b.take<uint8_t>(DEPOSIT_DATA_BYTES * n);
+  uint8_t* d_dom = b.take<uint8_t>(8 * n);
+  uint8_t* d_ver = b.take<uint8_t>(n);
+  uint8_t* d_ws = b.take<uint8_t>(wsb);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_dd, deposit_data, DEPOSIT_DATA_BYTES * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_dom, dom8s, 8 * n, hipMemcpyHostToDevice, s));
+  if ((rc = bls381_verify_deposits_device(n, d_dd, d_dom, d_ver, d_ws, s))) return rc;
+  HIPC(hipMemcpyAsync(verdicts, d_ver, n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
 }  // extern "C"

@@ -8,6 +8,7 @@
 //                    base[(c*14 + k) * 2n + 2i + p]   (lane index 2i + p)
 #pragma once
 #include "bls381_pair.hpp"
+#include "bls381_ssz.hpp"
 
 namespace bls381 {
 
@@ -401,6 +402,31 @@ __global__ void __launch_bounds__(KBLOCK) k_reg_lookup(size_t n, const uint8_t* 
     if (reg_key_eq(keys + 48 * (size_t)cur, k)) { r = (int32_t)cur; break; }
   }
   entry[t] = r;
+}
+
+// ------------------------------------------------------ SSZ roots (§8(f)2) --
+// roots of n serialized fixed-size items (item i at items + i * stride); the
+// program (bls381_ssz.hpp) is uniform, so every lane runs the same ops
+__global__ void __launch_bounds__(KBLOCK) k_ssz_root(size_t n, const uint8_t* __restrict__ items, size_t stride,
+                                                     const uint32_t* __restrict__ prog, uint32_t plen,
+                                                     uint8_t* __restrict__ roots, int32_t* __restrict__ err) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  uint32_t stk[SSZ_STACK][8];
+  uint32_t r[8];
+  if (!ssz_run(r, items + i * stride, prog, plen, stk)) { *err = 1; return; }
+  uint8_t* o = roots + 32 * i;
+  for (int w = 0; w < 8; ++w)
+    for (int b = 0; b < 4; ++b) o[4 * w + b] = (uint8_t)(r[w] >> (24 - 8 * b));
+}
+
+// gather a byte field [off, off + len) of n strided items into a packed array
+__global__ void __launch_bounds__(KBLOCK) k_gather_field(size_t n, const uint8_t* __restrict__ items, size_t stride,
+                                                         uint32_t off, uint32_t len, uint8_t* __restrict__ out) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * len) return;
+  const size_t i = t / len, b = t % len;
+  out[t] = items[i * stride + off + b];
 }
 
 // ------------------------------------------------------- sign / privtopub --

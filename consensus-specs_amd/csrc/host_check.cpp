@@ -13,6 +13,7 @@
 
 #include "bls381_hash.hpp"
 #include "bls381_pairing.hpp"
+#include "bls381_ssz.hpp"
 
 using namespace bls381;
 
@@ -142,6 +143,16 @@ void hc_g1_mul(const uint8_t* aff96, const uint32_t* k_limbs, int nbits, uint8_t
 }
 void hc_g2_mul(const uint8_t* aff192, const uint32_t* k_limbs, int nbits, uint8_t* b96) {
   g2_compress(b96, jac_mul_limbs(ldg2(aff192), k_limbs, nbits));
+}
+
+// SSZ root program (bls381_ssz.hpp) over one serialized item: 1 ok, 0 malformed program
+int hc_ssz_root(const uint8_t* item, const uint32_t* prog, uint32_t plen, uint8_t* out32) {
+  static uint32_t stk[SSZ_STACK][8];
+  uint32_t r[8];
+  if (!ssz_run(r, item, prog, plen, stk)) return 0;
+  for (int w = 0; w < 8; ++w)
+    for (int b = 0; b < 4; ++b) out32[4 * w + b] = (uint8_t)(r[w] >> (24 - 8 * b));
+  return 1;
 }
 
 #if defined(BLS_COUNT_OPS)

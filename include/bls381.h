@@ -175,6 +175,33 @@ int bls381_registry_aggregate_indices_device(bls381_registry* reg, size_t n_grou
                                              size_t n_idx, const uint32_t* d_indices, uint8_t* d_out48,
                                              int32_t* d_status, void* d_workspace, void* stream);
 
+/* ---- SSZ roots: the message_hash producer ---------- */
+/* hash_tree_root / signing_root of n serialized fixed-size SSZ items
+ * (test_libs/pyspec/eth2spec/utils/ssz/ssz_impl.py:143-163, merkle_minimal.py
+ * merkleize_chunks).  `prog` is the item type compiled by bls381_amd/ssz.py:
+ * words {1, off, len} push bytes [off, off+len) zero-padded to a 32-byte chunk
+ * (len <= 32); {2, k} merkleizes the top k chunks (zero-padded to a power of
+ * two) into one.  The program must leave exactly one chunk, read only inside
+ * the item, and fit 512 words / 64 chunks, else BLS381_EARG.  roots32 receives
+ * n x 32 bytes. */
+int bls381_ssz_root_batch(size_t n, const uint8_t* items, size_t item_size, const uint32_t* prog,
+                          uint32_t prog_len, uint8_t* roots32);
+size_t bls381_ssz_root_workspace_size(void);
+/* Device form: item i at d_items + i * stride (stride >= item_size); h_prog on the host. */
+int bls381_ssz_root_batch_device(size_t n, const uint8_t* d_items, size_t stride, size_t item_size,
+                                 const uint32_t* h_prog, uint32_t prog_len, uint8_t* d_roots32,
+                                 void* d_workspace, void* stream);
+/* process_deposit's proof-of-possession check over n serialized DepositData
+ * (184 B each: pubkey, withdrawal_credentials, amount, signature;
+ * 0_beacon-chain.md:394-403): verdicts[i] = bls_verify(pubkey,
+ * signing_root(deposit.data), signature, domain) (0_beacon-chain.md:1755-1758),
+ * the signing roots computed on the device and fed straight to the verify
+ * pipeline. */
+int bls381_verify_deposits(size_t n, const uint8_t* deposit_data, const uint8_t* dom8s, uint8_t* verdicts);
+size_t bls381_verify_deposits_workspace_size(size_t n);
+int bls381_verify_deposits_device(size_t n, const uint8_t* d_deposit_data, const uint8_t* d_dom8s,
+                                  uint8_t* d_verdicts, void* d_workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

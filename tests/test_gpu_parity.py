@@ -504,3 +504,50 @@ def test_yaml_vectors_generate_and_run(native, golden, tmp_path):
     V.write_suites(str(tmp_path), cases)
     res = V.run(str(tmp_path), bls)
     assert sum(ok for ok, _ in res.values()) == 94 and not any(f for _, f in res.values())
+
+
+# ------------------------------------------------ SSZ roots (§8(f) rank 2)
+def test_ssz_roots_match_fixtures(native, golden):
+    import json
+    from bls381_amd import ssz
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ssz_roots.json")) as f:
+        fx = json.load(f)
+    types = {"DepositData": ssz.DepositData, "AttestationDataAndCustodyBit": ssz.AttestationDataAndCustodyBit,
+             "AttestationData": ssz.AttestationData, "Crosslink": ssz.Crosslink,
+             "BeaconBlockHeader": ssz.BeaconBlockHeader}
+    for name, typ in types.items():
+        cases = [c for c in fx["roots"] if c["type"] == name]
+        items = [bytes.fromhex(c["serialized"]) for c in cases] * 50          # a batch of several waves
+        got = ssz.hash_tree_root_batch(typ, items)
+        assert [g.hex() for g in got] == [c["hash_tree_root"] for c in cases] * 50, name
+        got = ssz.signing_root_batch(typ, items)
+        assert [g.hex() for g in got] == [c["signing_root"] for c in cases] * 50, name
+
+
+def test_verify_deposits_pipeline(native):
+    """process_deposit's PoP check with signing roots made on the device == oracle verdicts."""
+    import ssz_oracle as S
+    from bls381_amd import bls, ssz
+    rng = random.Random(0xB15_0008)
+    dom = 3
+    items, want = [], []
+    for j in range(300):
+        sk = rng.randrange(1, 1 << 250)
+        v = {"pubkey": bls.privtopub(sk), "withdrawal_credentials": bytes(rng.randrange(256) for _ in range(32)),
+             "amount": 32 * 10 ** 9 + j, "signature": b"\x00" * 96}
+        root = S.signing_root(S.DepositData, v)
+        v["signature"] = bls.bls_sign(root, sk, dom)
+        ok = True
+        if j % 7 == 3:
+            v["amount"] += 1; ok = False             # signed data changed
+        elif j % 7 == 5:
+            v["signature"] = b"\x00" * 96; ok = False
+        items.append(S.serialize(S.DepositData, v))
+        want.append(ok)
+    got = ssz.verify_deposits(items, dom)
+    assert list(got) == want
+    for k in (0, 3, 5):                                # the oracle's own verify on a few
+        v = items[k]
+        assert O.verify(S.signing_root(S.DepositData, {"pubkey": v[:48], "withdrawal_credentials": v[48:80],
+                                                       "amount": int.from_bytes(v[80:88], "little"),
+                                                       "signature": v[88:]}), v[:48], v[88:], dom) == want[k]
