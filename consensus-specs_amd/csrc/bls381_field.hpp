@@ -262,7 +262,8 @@ BLS_HD inline fp_t fp_pow_qm3d4(const fp_t& a) {
   return r;
 }
 
-BLS_HD inline fp_t fp_inv(const fp_t& a) { return fp_mul(fp_sqr(fp_sqr(fp_pow_qm3d4(a))), a); }
+// (fp_inv: binary extended gcd, below the word helpers)
+BLS_HD inline fp_t fp_inv(const fp_t& a);
 
 // returns true and sets r when a is a square; r = a^((q+1)/4)
 BLS_HD inline bool fp_sqrt(fp_t& r, const fp_t& a) {
@@ -431,6 +432,121 @@ BLS_HD inline int fp_legendre(const fp_t& am) {
   for (int i = 1; i < 12; ++i) one |= n[i];
   if (one != 0) return 0;
   return t ? -1 : 1;
+}
+
+// ------------------------------------------------ inversion (binary xgcd) --
+BLS_INLINE uint32_t add_carry(uint32_t a, uint32_t b, uint32_t cin, uint32_t& cout) {
+#if defined(__clang__)
+  unsigned int co;
+  const uint32_t r = __builtin_addc(a, b, cin, &co);
+  cout = co;
+  return r;
+#else
+  const uint64_t v = (uint64_t)a + b + cin;
+  cout = (uint32_t)(v >> 32);
+  return (uint32_t)v;
+#endif
+}
+
+// x / 2^k mod q for x < 2q and 1 <= k <= 31: (x + m q) / 2^k with
+// m = -x q^-1 mod 2^k, an exact shift; the result stays < 2q
+BLS_INLINE void words_div2k_modq(uint32_t x[12], uint32_t k) {
+  const uint32_t m = (x[0] * Q_NINV32) & ((1u << k) - 1u);
+  uint32_t t[13];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    c += (uint64_t)m * Q_WORDS[i] + x[i];
+    t[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  t[12] = (uint32_t)c;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x[i] = (uint32_t)((((uint64_t)t[i + 1] << 32) | t[i]) >> k);
+}
+
+// d = a - b mod 2q for a, b < 2q; d in [0, 2q)
+BLS_INLINE void words_sub_mod2q(uint32_t d[12], const uint32_t a[12], const uint32_t b[12]) {
+  uint32_t br = 0, c = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d[i] = sub_borrow(a[i], b[i], br, br);
+  const uint32_t mask = 0u - br;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) d[i] = add_carry(d[i], Q2_WORDS[i] & mask, c, c);
+}
+
+// u >>= (its factors of two), x /= 2^(the same count) mod q
+BLS_INLINE void xgcd_strip(uint32_t u[12], uint32_t x[12]) {
+  while (u[0] == 0) {   // a whole zero word: probability ~2^-32 per step
+#pragma unroll
+    for (int i = 0; i < 11; ++i) u[i] = u[i + 1];
+    u[11] = 0;
+    words_div2k_modq(x, 16);
+    words_div2k_modq(x, 16);
+  }
+  const uint32_t k = (uint32_t)__builtin_ctz(u[0]);
+  if (k) {
+    words_shr(u, k);
+    words_div2k_modq(x, k);
+  }
+}
+
+// 12 x 32-bit words (value < 2^381) -> 14 x 28-bit limbs
+BLS_INLINE fp_t fp_from_words(const uint32_t w[12]) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int bit = 28 * k, i = bit / 32, sh = bit % 32;
+    uint32_t v = w[i] >> sh;
+    if (sh > 4 && i + 1 < 12) v |= w[i + 1] << (32 - sh);
+    r.w[k] = v & FP_MASK;
+  }
+  return r;
+}
+
+// 1/a (0 -> 0).  Binary extended gcd on the integer A = aR mod q, the same loop
+// shape as fp_legendre (one subtraction, a conditional swap, one strip of twos
+// per step, ~270 steps of ~150 word ops), then A^-1 R^3 R^-1 = a^-1 R by one
+// Montgomery product.  Several times cheaper than a^(q-2) (453 Fp products).
+// Invariants: x1 A = u, x2 A = v (mod q); u, v odd after each strip; x1, x2 < 2q.
+BLS_HD inline fp_t fp_inv(const fp_t& am) {
+  uint32_t u[12], v[12], x1[12], x2[12];
+  fp_plain_to_words(u, fp_reduce_once(am));
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) z |= u[i];
+  if (z == 0) return fp_zero();
+#pragma unroll
+  for (int i = 0; i < 12; ++i) { v[i] = Q_WORDS[i]; x1[i] = 0; x2[i] = 0; }
+  x1[0] = 1;
+  xgcd_strip(u, x1);
+  while (true) {
+    uint32_t d[12], br = 0, nz = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) { d[i] = sub_borrow(u[i], v[i], br, br); nz |= d[i]; }
+    if (nz == 0) break;                 // u == v == gcd == 1
+    // u > v: (u, x1) <- (u - v, x1 - x2);  u < v: (u, v, x1, x2) <- (v - u, u, x2 - x1, x1)
+    uint32_t xd[12], xn[12], nb = 0;
+    words_sub_mod2q(xd, x1, x2);
+    words_sub_mod2q(xn, x2, x1);
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const uint32_t nd = sub_borrow(0u, d[i], nb, nb);
+      const uint32_t uo = u[i], xo = x1[i];
+      u[i] = br ? nd : d[i];
+      v[i] = br ? uo : v[i];
+      x1[i] = br ? xn[i] : xd[i];
+      x2[i] = br ? xo : x2[i];
+    }
+    xgcd_strip(u, x1);
+  }
+  // x1 < 2q -> canonical
+  uint32_t e[12], bq = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) e[i] = sub_borrow(x1[i], Q_WORDS[i], bq, bq);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) x1[i] = bq ? x1[i] : e[i];
+  return fp_mul(fp_from_words(x1), FP_R3);
 }
 
 // ---------------------------------------------------------------- Fp2 -----

@@ -242,3 +242,21 @@ def test_scalar_mul_fixture_helpers(L):
     limbs = (ctypes.c_uint32 * 8)(*[(k >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
     L.hc_g1_mul(b48(O.g_x) + b48(O.g_y), limbs, 256, out)
     assert out.raw == O.privtopub(k)
+
+
+def test_fp_inv_binary_xgcd_edges(L):
+    """fp_inv (binary extended gcd on the Montgomery integer): random values and values whose
+    Montgomery form has long runs of factors of two or sits next to q; 0 -> 0."""
+    R = 1 << 392
+    rinv = pow(R, -1, q)
+    rng = random.Random(61)
+    buf = ctypes.create_string_buffer(48)
+    vals = [1, 2, q - 1, q - 2, (q + 1) // 2, 3]
+    # a whose Montgomery integer aR mod q is 2^k (k up to 380, including >= 32 zero low bits)
+    vals += [(1 << k) * rinv % q for k in (1, 31, 32, 33, 64, 100, 200, 380)]
+    vals += [rng.randrange(1, q) for _ in range(1500)]
+    for a in vals:
+        L.hc_fp_inv(b48(a), buf)
+        assert i48(buf.raw) * a % q == 1, a
+    L.hc_fp_inv(b48(0), buf)
+    assert i48(buf.raw) == 0
