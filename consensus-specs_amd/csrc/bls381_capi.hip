@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <type_traits>
 #include <vector>
 
 #include "bls381.h"
@@ -230,6 +231,8 @@ struct AggPlan {
   std::vector<std::vector<agg_chunk>> levels;   // chunks per level
 };
 constexpr uint32_t CHUNK_L1 = 4 * KBLOCK;
+// level-1 chunks averaging fewer inputs than this are summed one lane per chunk (k_agg_lanes)
+constexpr size_t AGG_LANE_AVG_MAX = 8;
 constexpr uint32_t CHUNK_LN = 4 * KBLOCK;
 
 AggPlan plan_agg(size_t ng, const uint32_t* offsets) {
@@ -282,7 +285,13 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
     uint8_t* bad = b.take<uint8_t>(lv.size());
     HIPC(hipMemcpyAsync(d_chunks, lv.data(), lv.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
     const agg_reg_src none{nullptr, nullptr, nullptr, 0, 0};
-    if (l == 0 && reg) {
+    size_t n_in_total = 0;
+    for (const auto& ch : lv) n_in_total += ch.end - ch.begin;
+    const bool lanes = std::is_same<F, fp_t>::value && l == 0 && n_in_total < AGG_LANE_AVG_MAX * lv.size();
+    if (lanes) {
+      LAUNCH("agg_lane_sum", s, dim3(grid_for(lv.size())), dim3(KBLOCK), k_agg_lanes<AGG_REGISTRY>, (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, d_in, jac, bad, reg ? *reg : none);
+    } else if (l == 0 && reg) {
       LAUNCH("agg_registry_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_REGISTRY>),
              (size_t)lv.size(), (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0,
              (const uint8_t*)nullptr, jac, bad, *reg);

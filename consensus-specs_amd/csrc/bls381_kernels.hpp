@@ -230,6 +230,44 @@ struct agg_reg_src {
   size_t size;            // entries in use: an entry >= size is an error (BAD), never read
 };
 
+// adds level-1 input e (compressed bytes, or a registry entry) to acc
+template <class F, int MODE>
+__device__ __forceinline__ void agg_accumulate(jac_t<F>& acc, bool& bad, uint32_t e, const uint8_t* in_bytes,
+                                               const agg_reg_src& reg) {
+  if (MODE == AGG_REGISTRY) {
+    const int32_t r = reg.entry ? reg.entry[e] : -1;
+    if ((r >= 0 && (size_t)r >= reg.size) || (r < 0 && !in_bytes)) { bad = true; return; }
+    if (r >= 0) {
+      const uint8_t rs = reg.st[r];
+      if (rs == ST_BAD) bad = true;
+      else if (rs == ST_OK) acc = jac_add_aff(acc, reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r));
+      return;
+    }
+  }
+  aff_t<F> a;
+  const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
+  if (s == PT_BAD) bad = true;
+  else if (s == PT_OK) acc = jac_add_aff(acc, a);
+}
+
+// Level 1 for small G1 chunks: one lane sums one chunk in sequence.  Used when
+// chunks average a few inputs (bls_verify_multiple's per-message groups, often
+// one key each), where a workgroup per chunk would leave 127 of 128 lanes idle.
+template <int MODE>
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_lanes(size_t nchunks, const agg_chunk* __restrict__ chunks,
+                                                     const uint8_t* __restrict__ in_bytes,
+                                                     uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad,
+                                                     agg_reg_src reg) {
+  const size_t c = item_index<1>();
+  if (c >= nchunks) return;
+  const agg_chunk ch = chunks[c];
+  jac_t<fp_t> acc = jac_infinity<fp_t>();
+  bool bad = false;
+  for (uint32_t e = ch.begin; e < ch.end; ++e) agg_accumulate<fp_t, MODE>(acc, bad, e, in_bytes, reg);
+  soa_jac<fp_t>::st(out_jac, nchunks, c, acc);
+  out_bad[c] = bad ? 1 : 0;
+}
+
 template <class F, int MODE>
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                       const uint8_t* __restrict__ in_bytes,
@@ -255,20 +293,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t 
       acc = jac_add(acc, soa_jac<F>::ld(in_jac, n_in, e));
       continue;
     }
-    if (MODE == AGG_REGISTRY) {
-      const int32_t r = reg.entry ? reg.entry[e] : -1;
-      if ((r >= 0 && (size_t)r >= reg.size) || (r < 0 && !in_bytes)) { bad = true; continue; }
-      if (r >= 0) {
-        const uint8_t rs = reg.st[r];
-        if (rs == ST_BAD) bad = true;
-        else if (rs == ST_OK) acc = jac_add_aff(acc, reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r));
-        continue;
-      }
-    }
-    aff_t<F> a;
-    const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
-    if (s == PT_BAD) bad = true;
-    else if (s == PT_OK) acc = jac_add_aff(acc, a);
+    agg_accumulate<F, MODE>(acc, bad, e, in_bytes, reg);
   }
   if (bad) bad_any = 1;
   // tree reduction through LDS (lane-major words: conflict-free stride-1 access);
