@@ -134,16 +134,22 @@ BLS_INLINE jac_t<E> g2_psi_jac(const jac_t<E>& p) {
 //   Q_i = (-psi)^i BP(P).
 // ~190 doublings + ~45 additions instead of the 508-doubling ladder; the
 // identity is checked in oracle/tower_model.py and tests/test_tower_model.py.
-// [e0] S by the NAF of e0 (leading digit +1); one call, loop body inlined
+// [e0] S by the NAF of e0 (leading digit +1); one call, loop body inlined.  S is
+// made affine first (one Fp2 inversion, a binary-xgcd Fp inverse): each of the
+// NAF's additions is then a mixed addition (7M + 4S instead of 11M + 5S).
 template <class E>
 BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E>& S) {
-  const jac_t<E> nS = jac_neg(S);
-  jac_t<E> R = S;
+  aff_t<E> a;
+  if (!jac_to_aff(a, S)) return S;   // S = O: [e0] O = O
+  aff_t<E> na;
+  na.x = a.x;
+  na.y = f_neg(a.y);
+  jac_t<E> R = jac_from_aff(a);
   for (int i = 1; i < E0_NAF_LEN; ++i) {
     R = jac_dbl(R);
     const int dg = E0_NAF[i];
-    if (dg > 0) R = jac_add(R, S);
-    else if (dg < 0) R = jac_add(R, nS);
+    if (dg > 0) R = jac_add_aff(R, a);
+    else if (dg < 0) R = jac_add_aff(R, na);
   }
   return R;
 }
