@@ -348,10 +348,63 @@ def bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist):
         step()
     torch.cuda.synchronize()
     t = _max_time(time.perf_counter() - t0, world, dist, dev)
-    return {"workload": "C4: %d pubkeys per GPU (%d total) -> one bls_aggregate_pubkeys; per-GPU partial, "
-                        "all-gather, sum on rank 0" % (k, k * world),
+    out = {"workload": "C4: %d pubkeys per GPU (%d total) -> one bls_aggregate_pubkeys; per-GPU partial, "
+                       "all-gather, sum on rank 0" % (k, k * world),
+           "pubkeys_aggregated_per_s": k * world * steps / t, "ms_per_aggregate": 1e3 * t / steps,
+           "n_gpus": world}
+    out["registry"] = bench_c4_registry(native, L, args, world, rank, dev, stream, t_u8, dist)
+    return out
+
+
+def bench_c4_registry(native, L, args, world, rank, dev, stream, t_u8, dist):
+    """C4 from the device-resident registry: this rank's shard of the validator registry (k distinct keys,
+    decoded once) aggregated by validator index; partial per GPU, all-gather, sum on rank 0."""
+    import torch
+    from bls381_amd.registry import PubkeyRegistry
+    k = args.c4_keys
+    rng = np.random.default_rng(0xB15_0004 + rank)
+    sks = [int.from_bytes(rng.bytes(32), "big") % (R_ORDER - 1) + 1 for _ in range(k)]
+    pks = native.privtopub_batch(b"".join(x.to_bytes(32, "big") for x in sks))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reg = PubkeyRegistry(k)
+    ent = reg.add([pks[48 * i:48 * i + 48] for i in range(k)])
+    build = time.perf_counter() - t0
+    assert np.all(ent == np.arange(k))
+    off = np.array([0, k], dtype=np.uint32)
+    d_idx = t_u8(np.arange(k, dtype=np.uint32).tobytes())
+    d_out = torch.zeros(48, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(1, dtype=torch.int32, device=dev)
+    ws = torch.empty(L.bls381_registry_aggregate_workspace_size(1, k), dtype=torch.uint8, device=dev)
+    want_local = native.privtopub_batch((sum(sks) % R_ORDER).to_bytes(32, "big"))
+
+    def step():
+        native.check(L.bls381_registry_aggregate_indices_device(
+            reg._h, 1, off.ctypes.data_as(ctypes.c_void_p), k, d_idx.data_ptr(), d_out.data_ptr(), d_st.data_ptr(),
+            ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        if world > 1:
+            parts = [torch.empty_like(d_out) for _ in range(world)]
+            dist.all_gather(parts, d_out)
+            allp = torch.cat(parts).cpu().numpy().tobytes()
+        else:
+            allp = d_out.cpu().numpy().tobytes()
+        return allp, (native.aggregate_pubkeys(allp) if rank == 0 else None)
+
+    allp, _ = step()
+    assert allp[48 * rank:48 * rank + 48] == want_local, "C4 registry aggregate mismatch"
+    steps = max(args.steps, 3) * 4
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    t = _max_time(time.perf_counter() - t0, world, dist, dev)
+    reg.close()
+    return {"workload": "C4 from per-GPU registry shards of %d decoded pubkeys, aggregated by index" % k,
             "pubkeys_aggregated_per_s": k * world * steps / t, "ms_per_aggregate": 1e3 * t / steps,
-            "n_gpus": world}
+            "registry_build_ms": 1e3 * build}
 
 
 def bench_c5(native, args, world, rank, dist, dev):
