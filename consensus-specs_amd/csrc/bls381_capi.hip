@@ -448,8 +448,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_chunk_product
 
 // Runs a planned batch up to (and excluding) the final exponentiation.  Returns
 // per-call Fp12 products and statuses (SoA over n_calls) on the device.
-int run_vm_batch(const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hipStream_t s, uint32_t** out_f,
-                 uint8_t** out_st) {
+int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hipStream_t s,
+                 uint32_t** out_f, uint8_t** out_st) {
   const size_t G = pl.G, ncalls = pl.n_calls, np = pl.npairs;
   uint8_t* d_pks = b.take<uint8_t>(pl.pks_perm.size() + 1);
   uint8_t* d_msgs = b.take<uint8_t>(pl.group_msg.size() + 1);
@@ -461,27 +461,40 @@ int run_vm_batch(const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hi
   if (!pl.group_dom.empty()) HIPC(hipMemcpyAsync(d_doms, pl.group_dom.data(), pl.group_dom.size(), hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * ncalls, hipMemcpyHostToDevice, s));
   if (np) HIPC(hipMemcpyAsync(d_src, pl.pair_src.data(), np * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  // group sums -> affine + subgroup check
+  // Small batches (an epoch's attestations, one custody call) leave most of the
+  // GPU idle, so the independent stages overlap: the pubkey-group sums and the
+  // signature decodes run on the side stream while the main stream hashes the
+  // messages; the Miller loops wait for both.
   uint32_t* agg_aff = b.take<uint32_t>(2 * FP_LIMBS * (G + 1));
   uint8_t* agg_st = b.take<uint8_t>(G + 1);
   uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
   uint8_t* h_st = b.take<uint8_t>(G + 1);
-  if (G > 0) {
-    const uint32_t* jac;
-    const uint8_t* bad;
-    size_t used = 0;
-    uint8_t* sub = b.take<uint8_t>(0);
-    int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, s, &jac, &bad, &used, b.left());
-    if (rc) return rc;
-    b.off += used;
-    LAUNCH("agg_g1_affine", s, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
-    LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs, (uint32_t)mlen,
-           (const uint8_t*)d_doms, 8, h_aff, h_st);
-  }
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
-  LAUNCH("decode_g2", s, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs, sig_aff,
-         sig_st, 1);
+  {
+    std::lock_guard<std::mutex> fk(c->fork_mu);
+    hipStream_t side = c->side;
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(side, c->ev_fork, 0));
+    if (G > 0) {
+      // group sums -> affine + subgroup check
+      const uint32_t* jac;
+      const uint8_t* bad;
+      size_t used = 0;
+      uint8_t* sub = b.take<uint8_t>(0);
+      int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, side, &jac, &bad, &used, b.left());
+      if (rc) return rc;
+      b.off += used;
+      LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
+    }
+    LAUNCH("decode_g2", side, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs,
+           sig_aff, sig_st, 1);
+    HIPC(hipEventRecord(c->ev_join, side));
+    if (G > 0)
+      LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs,
+             (uint32_t)mlen, (const uint8_t*)d_doms, 8, h_aff, h_st);
+    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+  }
   uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * (np + 1));
   uint8_t* st = b.take<uint8_t>(np + 1);
   if (np)
@@ -674,7 +687,7 @@ int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const
   Bump b(c->ws, c->ws_cap);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = run_vm_batch(pl, msg_len, sigs, b, c->stream, &f, &st))) return rc;
+  if ((rc = run_vm_batch(c, pl, msg_len, sigs, b, c->stream, &f, &st))) return rc;
   uint8_t* d_v = b.take<uint8_t>(n_calls);
   LAUNCH("final_exp", c->stream, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
          (const uint32_t*)f, (const uint8_t*)st, d_v);
@@ -709,7 +722,7 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
   Bump b(c->ws, c->ws_cap);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = run_vm_batch(pl, msg_len, sig, b, c->stream, &f, &st))) return rc;
+  if ((rc = run_vm_batch(c, pl, msg_len, sig, b, c->stream, &f, &st))) return rc;
   uint8_t* d_out = b.take<uint8_t>(576);
   LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(KBLOCK), k_fp12_to_bytes, (size_t)1, (const uint32_t*)f, d_out);
   uint8_t h_st = 0;
