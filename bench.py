@@ -110,7 +110,8 @@ def load_pmc_traffic(prof_key, n):
     runs of tools/prof_workload.py at the same n; FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM").
     PMC counters cannot be read inside the timed run, so this is the last profiled build's figure."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_counters.json")), key=os.path.getmtime)
+    # newest by round tag (pmc_r01a < pmc_r01h ...): file mtimes are not preserved by a checkout
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_counters.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
