@@ -8,8 +8,11 @@
 // keep the scheduler from interleaving independent phases (bounds live ranges)
 #if defined(__HIP_DEVICE_COMPILE__)
 #define BLS_PHASE() __builtin_amdgcn_sched_barrier(0)
+// true on every active lane when c holds on any of them (a wave-uniform branch)
+#define BLS_ANY(c) (__builtin_amdgcn_ballot_w64((c)) != 0)
 #else
 #define BLS_PHASE() ((void)0)
+#define BLS_ANY(c) (c)
 #endif
 #define BLS_HD __host__ __device__
 #define BLS_INLINE __host__ __device__ __forceinline__
@@ -17,6 +20,7 @@
 #define BLS_CONST __device__ __constant__ static constexpr
 #else
 #define BLS_PHASE() ((void)0)
+#define BLS_ANY(c) (c)
 #define BLS_HD
 #define BLS_INLINE inline __attribute__((always_inline))
 #define BLS_NOINLINE __attribute__((noinline))

@@ -37,46 +37,115 @@ BLS_INLINE void fp_carry(int32_t (&t)[14]) {
   }
 }
 
-// given s (value < 4q, limbs < 2^29): return s mod 2q in normalized form
-BLS_INLINE fp_t fp_fold_2q(const int32_t (&s)[14]) {
-  int32_t a[14], b[14];
+// One reduction per linear combination (DESIGN.md "Arithmetic").  s is a
+// non-negative combination of normalized values -- limbs 0..12 in [0, 2^31 - 8],
+// the top limb >= -2 (a subtracted top limb may exceed the borrowed constant's by
+// up to 2), value in [0, KMAX * 2q) with KMAX <= 8 -- and the result is s mod 2q,
+// normalized: the unique value in [0, 2q), so bit-identical to any chain of
+// two-operand additions and subtractions over the same terms.
+//   k = floor(s13 / (Q2_13 + 1)) is at most floor(s / 2q) (no carry has been
+//   propagated into limb 13 yet, and 2q < (Q2_13 + 1) 2^364) and at least
+//   floor(s / 2q) - 1 (the carries into limb 13 are <= 8), so after s - k 2q and
+//   one carry pass the value is in [0, 4q).  A value >= 2q has top limb >= Q2_13;
+//   that (about one lane in 2^14) takes the exact conditional subtraction under a
+//   wave-uniform branch.
+template <int KMAX>
+BLS_INLINE fp_t fp_reduce_lc(const uint32_t (&s)[14]) {
+  static_assert(KMAX >= 1 && KMAX <= 8, "value bound");
+  int32_t t[14];
+  if (KMAX <= 2) {          // k in {0, 1}
+    const uint32_t m = (int32_t)s[13] > (int32_t)Q2_LIMBS[13] ? ~0u : 0u;
 #pragma unroll
-  for (int i = 0; i < 14; ++i) { a[i] = s[i]; b[i] = s[i] - (int32_t)Q2_LIMBS[i]; }
-  fp_carry(a);
-  fp_carry(b);
-  const bool neg = b[13] < 0;   // s < 2q
-  fp_t r;
+    for (int i = 0; i < 14; ++i) t[i] = (int32_t)(s[i] - (Q2_LIMBS[i] & m));
+  } else {                  // k <= 7: s_i - k q2_i < 2^31 in magnitude
+    const int32_t top = (int32_t)s[13] > 0 ? (int32_t)s[13] : 0;   // < 0: value < 2q, k = 0
+    const uint32_t k = (uint32_t)(((uint64_t)(uint32_t)top * LC_DIV_MAGIC) >> 40);
 #pragma unroll
-  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(neg ? a[i] : b[i]);
-  return r;
-}
-
-BLS_INLINE fp_t fp_add(const fp_t& a, const fp_t& b) {
-  int32_t s[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) s[i] = (int32_t)(a.w[i] + b.w[i]);
-  return fp_fold_2q(s);
-}
-
-// a - b for a, b < 2q: d in (-2q, 2q); add 2q when negative
-BLS_INLINE fp_t fp_sub(const fp_t& a, const fp_t& b) {
-  int32_t d[14], e[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    d[i] = (int32_t)a.w[i] - (int32_t)b.w[i];
-    e[i] = d[i] + (int32_t)Q2_LIMBS[i];
+    for (int i = 0; i < 14; ++i) t[i] = (int32_t)(s[i] + k * NQ2_LIMBS[i]);
   }
-  fp_carry(d);
-  fp_carry(e);
-  const bool neg = d[13] < 0;
+  fp_carry(t);
+  if (BLS_ANY(t[13] >= (int32_t)Q2_LIMBS[13])) {
+    int32_t e[14];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) e[i] = t[i] - (int32_t)Q2_LIMBS[i];
+    fp_carry(e);
+    const bool ge = e[13] >= 0;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) t[i] = ge ? e[i] : t[i];
+  }
   fp_t r;
 #pragma unroll
-  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(neg ? e[i] : d[i]);
+  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)t[i];
   return r;
 }
 
-BLS_INLINE fp_t fp_neg(const fp_t& a) { return fp_sub(fp_zero(), a); }
-BLS_INLINE fp_t fp_dbl(const fp_t& a) { return fp_add(a, a); }
+// a + b (< 4q)
+BLS_INLINE fp_t fp_add(const fp_t& a, const fp_t& b) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] + b.w[i];
+  return fp_reduce_lc<2>(s);
+}
+
+// a - b + 2q (in (0, 4q)); Q2B's limbs are >= 2^28 - 1 >= b's, so no limb goes negative
+BLS_INLINE fp_t fp_sub(const fp_t& a, const fp_t& b) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] + Q2B_LIMBS[i] - b.w[i];
+  return fp_reduce_lc<2>(s);
+}
+
+BLS_INLINE fp_t fp_neg(const fp_t& a) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = Q2B_LIMBS[i] - a.w[i];
+  return fp_reduce_lc<2>(s);
+}
+
+BLS_INLINE fp_t fp_dbl(const fp_t& a) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] << 1;
+  return fp_reduce_lc<2>(s);
+}
+
+// a + b - c (< 6q)
+BLS_INLINE fp_t fp_add_sub(const fp_t& a, const fp_t& b, const fp_t& c) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] + b.w[i] + Q2B_LIMBS[i] - c.w[i];
+  return fp_reduce_lc<3>(s);
+}
+
+// a + b + c (< 6q)
+BLS_INLINE fp_t fp_add3(const fp_t& a, const fp_t& b, const fp_t& c) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] + b.w[i] + c.w[i];
+  return fp_reduce_lc<3>(s);
+}
+
+// a - b - c + 4q (in (0, 6q)); Q4B's limbs are >= 2^29 - 2 >= b_i + c_i
+BLS_INLINE fp_t fp_sub2(const fp_t& a, const fp_t& b, const fp_t& c) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.w[i] + Q4B_LIMBS[i] - b.w[i] - c.w[i];
+  return fp_reduce_lc<3>(s);
+}
+
+// 3X - 2x + 4q (in (0, 10q)) and 3X + 2x (< 10q): Granger-Scott outputs
+BLS_INLINE fp_t fp_3m2(const fp_t& X, const fp_t& x) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = 3u * X.w[i] + Q4B_LIMBS[i] - (x.w[i] << 1);
+  return fp_reduce_lc<5>(s);
+}
+BLS_INLINE fp_t fp_3p2(const fp_t& X, const fp_t& x) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = 3u * X.w[i] + (x.w[i] << 1);
+  return fp_reduce_lc<5>(s);
+}
 
 // lazy sum for a multiplication operand only: limbs < 2^29, value < 4q
 BLS_INLINE fp_t fp_add_lazy(const fp_t& a, const fp_t& b) {
@@ -211,10 +280,14 @@ BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) { BLS_COUNT_FP_MUL(); return fp_mul_bod
 BLS_NOINLINE fp_t fp_sqr(fp_t a) { BLS_COUNT_FP_MUL(); return fp_sqr_body(a); }
 #endif
 
-// k * a for a small constant k (k * 2q < 2^31): limb scale, then reduce mod 2q
+// k * a for a small constant k: one reduction for k <= 8 (k a < 16q, limbs < 2^31)
 BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
-  // k*a < 2kq; fold by repeated conditional subtraction of 2q is k/2 steps --
-  // instead multiply by k in Montgomery form via an addition chain of fp_add
+  if (k <= 8) {
+    uint32_t s[14];
+#pragma unroll
+    for (int i = 0; i < 14; ++i) s[i] = (uint32_t)k * a.w[i];
+    return fp_reduce_lc<8>(s);
+  }
   fp_t r = a;
   fp_t acc = fp_zero();
   bool first = true;
@@ -557,7 +630,7 @@ BLS_INLINE bool fp2_eq(const fp2_t& a, const fp2_t& b) { return fp_eq(a.c0, b.c0
 BLS_INLINE fp2_t fp2_add(const fp2_t& a, const fp2_t& b) { fp2_t r; r.c0 = fp_add(a.c0, b.c0); r.c1 = fp_add(a.c1, b.c1); return r; }
 BLS_INLINE fp2_t fp2_sub(const fp2_t& a, const fp2_t& b) { fp2_t r; r.c0 = fp_sub(a.c0, b.c0); r.c1 = fp_sub(a.c1, b.c1); return r; }
 BLS_INLINE fp2_t fp2_neg(const fp2_t& a) { fp2_t r; r.c0 = fp_neg(a.c0); r.c1 = fp_neg(a.c1); return r; }
-BLS_INLINE fp2_t fp2_dbl(const fp2_t& a) { return fp2_add(a, a); }
+BLS_INLINE fp2_t fp2_dbl(const fp2_t& a) { fp2_t r; r.c0 = fp_dbl(a.c0); r.c1 = fp_dbl(a.c1); return r; }
 BLS_INLINE fp2_t fp2_half(const fp2_t& a) { fp2_t r; r.c0 = fp_half(a.c0); r.c1 = fp_half(a.c1); return r; }
 BLS_INLINE fp2_t fp2_conj(const fp2_t& a) { fp2_t r; r.c0 = a.c0; r.c1 = fp_neg(a.c1); return r; }
 BLS_INLINE fp2_t fp2_mul_fp(const fp2_t& a, const fp_t& b) { fp2_t r; r.c0 = fp_mul(a.c0, b); r.c1 = fp_mul(a.c1, b); return r; }
@@ -621,7 +694,7 @@ BLS_INLINE fp2_t fp2_mul(const fp2_t& a, const fp2_t& b) {
   const fp_t t2 = fp_mul(fp_add_lazy(a.c0, a.c1), fp_add_lazy(b.c0, b.c1));
   fp2_t r;
   r.c0 = fp_sub(t0, t1);
-  r.c1 = fp_sub(t2, fp_add(t0, t1));
+  r.c1 = fp_sub2(t2, t0, t1);
   return r;
 }
 
@@ -649,6 +722,23 @@ BLS_INLINE fp2_t fp2_mul_xi(const fp2_t& a) {
 
 BLS_INLINE fp2_t fp2_mul_small(const fp2_t& a, int k) {
   fp2_t r; r.c0 = fp_mul_small(a.c0, k); r.c1 = fp_mul_small(a.c1, k); return r;
+}
+
+// one-reduction combinations (fp_reduce_lc), shared names with the lane-pair type:
+// a + xi b = (a0 + b0 - b1) + (a1 + b0 + b1) u
+BLS_INLINE fp2_t fp2_add_mul_xi(const fp2_t& a, const fp2_t& b) {
+  fp2_t r; r.c0 = fp_add_sub(a.c0, b.c0, b.c1); r.c1 = fp_add3(a.c1, b.c0, b.c1); return r;
+}
+// a - b - c
+BLS_INLINE fp2_t fp2_sub2(const fp2_t& a, const fp2_t& b, const fp2_t& c) {
+  fp2_t r; r.c0 = fp_sub2(a.c0, b.c0, c.c0); r.c1 = fp_sub2(a.c1, b.c1, c.c1); return r;
+}
+// 3X - 2x and 3X + 2x
+BLS_INLINE fp2_t fp2_3m2(const fp2_t& X, const fp2_t& x) {
+  fp2_t r; r.c0 = fp_3m2(X.c0, x.c0); r.c1 = fp_3m2(X.c1, x.c1); return r;
+}
+BLS_INLINE fp2_t fp2_3p2(const fp2_t& X, const fp2_t& x) {
+  fp2_t r; r.c0 = fp_3p2(X.c0, x.c0); r.c1 = fp_3p2(X.c1, x.c1); return r;
 }
 
 BLS_HD inline fp2_t fp2_inv(const fp2_t& a) {
@@ -711,9 +801,9 @@ BLS_INLINE fp6_g<E> fp6_mul_inl(const fp6_g<E>& a, const fp6_g<E>& b) {
   const E t1 = fp2_mul(a.c1, b.c1);
   const E t2 = fp2_mul(a.c2, b.c2);
   fp6_g<E> r;
-  r.c0 = fp2_add(t0, fp2_mul_xi(fp2_sub(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b.c1, b.c2)), fp2_add(t1, t2))));
-  r.c1 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b.c0, b.c1)), fp2_add(t0, t1)), fp2_mul_xi(t2));
-  r.c2 = fp2_add(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), fp2_add(t0, t2)), t1);
+  r.c0 = fp2_add_mul_xi(t0, fp2_sub2(fp2_mul(fp2_add_lazy(a.c1, a.c2), fp2_add_lazy(b.c1, b.c2)), t1, t2));
+  r.c1 = fp2_add_mul_xi(fp2_sub2(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(b.c0, b.c1)), t0, t1), t2);
+  r.c2 = fp2_add(fp2_sub2(fp2_mul(fp2_add_lazy(a.c0, a.c2), fp2_add_lazy(b.c0, b.c2)), t0, t2), t1);
   return r;
 }
 
@@ -723,6 +813,20 @@ BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) { return fp6
 template <class E>
 BLS_INLINE fp6_g<E> fp6_mul_by_v(const fp6_g<E>& a) {
   fp6_g<E> r; r.c0 = fp2_mul_xi(a.c2); r.c1 = a.c0; r.c2 = a.c1; return r;
+}
+
+// a - b - c,  a + v b,  2a: one reduction per coefficient
+template <class E>
+BLS_INLINE fp6_g<E> fp6_sub2(const fp6_g<E>& a, const fp6_g<E>& b, const fp6_g<E>& c) {
+  fp6_g<E> r; r.c0 = fp2_sub2(a.c0, b.c0, c.c0); r.c1 = fp2_sub2(a.c1, b.c1, c.c1); r.c2 = fp2_sub2(a.c2, b.c2, c.c2); return r;
+}
+template <class E>
+BLS_INLINE fp6_g<E> fp6_add_mul_by_v(const fp6_g<E>& a, const fp6_g<E>& b) {
+  fp6_g<E> r; r.c0 = fp2_add_mul_xi(a.c0, b.c2); r.c1 = fp2_add(a.c1, b.c0); r.c2 = fp2_add(a.c2, b.c1); return r;
+}
+template <class E>
+BLS_INLINE fp6_g<E> fp6_dbl(const fp6_g<E>& a) {
+  fp6_g<E> r; r.c0 = fp2_dbl(a.c0); r.c1 = fp2_dbl(a.c1); r.c2 = fp2_dbl(a.c2); return r;
 }
 
 template <class E>
@@ -758,8 +862,8 @@ BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
   const fp6_g<E> ac = fp6_mul(a.c0, b.c0);
   const fp6_g<E> bd = fp6_mul(a.c1, b.c1);
   fp12_g<E> r;
-  r.c1 = fp6_sub(fp6_sub(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), ac), bd);
-  r.c0 = fp6_add(ac, fp6_mul_by_v(bd));
+  r.c1 = fp6_sub2(fp6_mul(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), ac, bd);
+  r.c0 = fp6_add_mul_by_v(ac, bd);
   return r;
 }
 
@@ -768,10 +872,10 @@ BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
 template <class E>
 BLS_INLINE fp12_g<E> fp12_sqr_inl(const fp12_g<E>& f) {
   const fp6_g<E> ab = fp6_mul_inl(f.c0, f.c1);
-  const fp6_g<E> t = fp6_mul_inl(fp6_add(f.c0, f.c1), fp6_add(f.c0, fp6_mul_by_v(f.c1)));
+  const fp6_g<E> t = fp6_mul_inl(fp6_add(f.c0, f.c1), fp6_add_mul_by_v(f.c0, f.c1));
   fp12_g<E> r;
-  r.c0 = fp6_sub(fp6_sub(t, ab), fp6_mul_by_v(ab));
-  r.c1 = fp6_add(ab, ab);
+  r.c0 = fp6_sub2(t, ab, fp6_mul_by_v(ab));
+  r.c1 = fp6_dbl(ab);
   return r;
 }
 
@@ -820,8 +924,8 @@ BLS_INLINE fp12_g<E> fp12_mul_by_line_inl(const fp12_g<E>& f, const E& c0, const
   {
     const E t0 = fp2_mul(a.c0, c0);
     const E t1 = fp2_mul(a.c1, c1);
-    aA.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(a.c2, c1)));
-    aA.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(c0, c1)), t0), t1);
+    aA.c0 = fp2_add_mul_xi(t0, fp2_mul(a.c2, c1));
+    aA.c1 = fp2_sub2(fp2_mul(fp2_add_lazy(a.c0, a.c1), fp2_add_lazy(c0, c1)), t0, t1);
     aA.c2 = fp2_add(t1, fp2_mul(a.c2, c0));
   }
   // bB, B = c2 v
@@ -836,13 +940,13 @@ BLS_INLINE fp12_g<E> fp12_mul_by_line_inl(const fp12_g<E>& f, const E& c0, const
   {
     const E t0 = fp2_mul(s.c0, c0);
     const E t1 = fp2_mul(s.c1, d1);
-    m.c0 = fp2_add(t0, fp2_mul_xi(fp2_mul(s.c2, d1)));
-    m.c1 = fp2_sub(fp2_sub(fp2_mul(fp2_add_lazy(s.c0, s.c1), fp2_add_lazy(c0, d1)), t0), t1);
+    m.c0 = fp2_add_mul_xi(t0, fp2_mul(s.c2, d1));
+    m.c1 = fp2_sub2(fp2_mul(fp2_add_lazy(s.c0, s.c1), fp2_add_lazy(c0, d1)), t0, t1);
     m.c2 = fp2_add(t1, fp2_mul(s.c2, c0));
   }
   fp12_g<E> r;
-  r.c0 = fp6_add(aA, fp6_mul_by_v(bB));
-  r.c1 = fp6_sub(fp6_sub(m, aA), bB);
+  r.c0 = fp6_add_mul_by_v(aA, bB);
+  r.c1 = fp6_sub2(m, aA, bB);
   return r;
 }
 
@@ -860,12 +964,12 @@ BLS_INLINE fp12_g<E> fp12_cyclotomic_sqr_inl(const fp12_g<E>& f) {
   auto sq4 = [](const E& x0, const E& x1, E& r0, E& r1) {
     const E t0 = fp2_sqr(x0);
     const E t1 = fp2_sqr(x1);
-    r0 = fp2_add(t0, fp2_mul_xi(t1));
-    r1 = fp2_sub(fp2_sqr(fp2_add(x0, x1)), fp2_add(t0, t1));
+    r0 = fp2_add_mul_xi(t0, t1);
+    r1 = fp2_sub2(fp2_sqr(fp2_add(x0, x1)), t0, t1);
   };
-  // 3X - 2x = X + 2(X - x) and 3X + 2x = X + 2(X + x): three additions each
-  auto m3s2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_sub(X, x))); };
-  auto m3a2 = [](const E& X, const E& x) { return fp2_add(X, fp2_dbl(fp2_add(X, x))); };
+  // 3X - 2x and 3X + 2x, one reduction each
+  auto m3s2 = [](const E& X, const E& x) { return fp2_3m2(X, x); };
+  auto m3a2 = [](const E& X, const E& x) { return fp2_3p2(X, x); };
   // Each group's outputs are formed as soon as its squares exist, so few Fp2
   // values stay live across the squaring calls (register pressure, not math).
   fp12_g<E> r;

@@ -55,27 +55,6 @@ __device__ __forceinline__ fp_t fp_sel(bool c, const fp_t& a, const fp_t& b) {
   return r;
 }
 
-// a + b (add) or a - b (!add) with the choice made per lane; inputs < 2q
-// normalized, output < 2q normalized.  One pass for both lanes of a pair whose
-// lanes need different signs (Fp2 multiplication by xi).
-__device__ __forceinline__ fp_t fp_addsub(const fp_t& a, const fp_t& b, bool add) {
-  const uint32_t m = add ? 0u : ~0u;   // b ^ m + s1 = +-b
-  const uint32_t s1 = add ? 0u : 1u;
-  int32_t d[14], e[14];
-#pragma unroll
-  for (int i = 0; i < 14; ++i) {
-    d[i] = (int32_t)(a.w[i] + (b.w[i] ^ m) + s1);
-    e[i] = d[i] + (int32_t)((Q2_LIMBS[i] ^ ~m) + (1u - s1));   // add: d - 2q, sub: d + 2q
-  }
-  fp_carry(d);
-  fp_carry(e);
-  const bool pick_e = add ? (e[13] >= 0) : (d[13] < 0);
-  fp_t r;
-#pragma unroll
-  for (int i = 0; i < 14; ++i) r.w[i] = (uint32_t)(pick_e ? e[i] : d[i]);
-  return r;
-}
-
 // ------------------------------------------------------ Fp2 multiplication --
 // lane 0: a0 b0 + a1 (8q - b1) = Re(ab);  lane 1: a1 b0 + a0 b1 = Im(ab).
 // Operands may be lazy sums (limbs < 2^29, values < 4q).  Column k holds <= 14
@@ -138,10 +117,29 @@ __device__ __forceinline__ fp2p_t fp2_add_lazy(const fp2p_t& a, const fp2p_t& b)
 __device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) { return pr_make(fp_mul(a.v, s)); }
 __device__ __forceinline__ fp2p_t fp2_mul_small(const fp2p_t& a, int k) { return pr_make(fp_mul_small(a.v, k)); }
 __device__ __forceinline__ fp2p_t fp2_conj(const fp2p_t& a) { return pr_make(fp_sel(pr_odd(), fp_neg(a.v), a.v)); }
-// xi = 1 + u:  (a0 - a1) + (a0 + a1) u
+// xi = 1 + u:  (a0 - a1) + (a0 + a1) u -- lane 0: a0 + (2q - a1), lane 1: a1 + a0
 __device__ __forceinline__ fp2p_t fp2_mul_xi(const fp2p_t& a) {
-  return pr_make(fp_addsub(a.v, pr_dpp<DPP_SWAP>(a.v), pr_odd()));
+  const bool odd = pr_odd();
+  const fp_t ao = pr_dpp<DPP_SWAP>(a.v);
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.v.w[i] + (odd ? ao.w[i] : Q2B_LIMBS[i] - ao.w[i]);
+  return pr_make(fp_reduce_lc<2>(s));
 }
+// a + xi b -- lane 0: a0 + b0 + (2q - b1), lane 1: a1 + b1 + b0 (one reduction)
+__device__ __forceinline__ fp2p_t fp2_add_mul_xi(const fp2p_t& a, const fp2p_t& b) {
+  const bool odd = pr_odd();
+  const fp_t bo = pr_dpp<DPP_SWAP>(b.v);
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) s[i] = a.v.w[i] + b.v.w[i] + (odd ? bo.w[i] : Q2B_LIMBS[i] - bo.w[i]);
+  return pr_make(fp_reduce_lc<3>(s));
+}
+__device__ __forceinline__ fp2p_t fp2_sub2(const fp2p_t& a, const fp2p_t& b, const fp2p_t& c) {
+  return pr_make(fp_sub2(a.v, b.v, c.v));
+}
+__device__ __forceinline__ fp2p_t fp2_3m2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3m2(X.v, x.v)); }
+__device__ __forceinline__ fp2p_t fp2_3p2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3p2(X.v, x.v)); }
 __device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
   return pr_make(fp_unpack(fp2p_mul_call(fp_pack(a.v), fp_pack(b.v))));
 }

@@ -38,6 +38,27 @@ aff_t<fp2_t> ldg2(const uint8_t* p) { aff_t<fp2_t> a; a.x = ld2(p); a.y = ld2(p 
 
 extern "C" {
 
+// one-reduction combinations on raw normalized limbs (14 x u32, values < 2q, Montgomery
+// or not -- the reduction is mod 2q only): op 0 a+b, 1 a-b, 2 -a, 3 2a, 4 a+b-c, 5 a+b+c,
+// 6 a-b-c, 7 3a-2b, 8 3a+2b, 9..16 k*a for k = op-8 (k = 1..8)
+void hc_fp_lc_raw(int op, const uint32_t* a, const uint32_t* b, const uint32_t* c, uint32_t* o) {
+  fp_t x, y, z, r;
+  for (int i = 0; i < 14; ++i) { x.w[i] = a[i]; y.w[i] = b[i]; z.w[i] = c[i]; }
+  switch (op) {
+    case 0: r = fp_add(x, y); break;
+    case 1: r = fp_sub(x, y); break;
+    case 2: r = fp_neg(x); break;
+    case 3: r = fp_dbl(x); break;
+    case 4: r = fp_add_sub(x, y, z); break;
+    case 5: r = fp_add3(x, y, z); break;
+    case 6: r = fp_sub2(x, y, z); break;
+    case 7: r = fp_3m2(x, y); break;
+    case 8: r = fp_3p2(x, y); break;
+    default: r = fp_mul_small(x, op - 8); break;
+  }
+  for (int i = 0; i < 14; ++i) o[i] = r.w[i];
+}
+
 void hc_fp_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_mul(ld(a), ld(b))); }
 void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_add(ld(a), ld(b))); }
 void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_sub(ld(a), ld(b))); }

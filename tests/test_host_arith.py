@@ -51,6 +51,43 @@ def test_fp_ops(L):
         assert v < 2 * q and v % q == a * b * Rinv % q
 
 
+def test_fp_one_reduction_combinations_raw(L):
+    """fp_reduce_lc (one reduction per linear combination) on raw limbs: the result is the
+    unique normalized value in [0, 2q) congruent to the combination mod 2q -- what the
+    two-operand add/sub chains it replaces return -- including inputs whose top limb
+    equals 2q's (the borrowed constants' top limb goes negative), and the rare lanes that
+    need the second subtraction."""
+    q2 = 2 * q
+    top2 = q2 >> 364
+    rng = random.Random(0x1C)
+    edge = [0, 1, q - 1, q, q + 1, q2 - 1, q2 - 2, top2 << 364, (top2 << 364) - 1, (1 << 364) - 1,
+            ((top2 - 1) << 364) + (1 << 363), q2 - (1 << 200)]
+    vals = edge + [rng.randrange(q2) for _ in range(300)]
+    # values just below multiples of 2q after combination: X near the 2q boundary
+    vals += [q2 - rng.randrange(1, 1 << 40) for _ in range(60)] + [rng.randrange(1 << 40) for _ in range(20)]
+    lim = lambda v: (ctypes.c_uint32 * 14)(*[(v >> (28 * i)) & ((1 << 28) - 1) for i in range(14)])
+    out = (ctypes.c_uint32 * 14)()
+    ops = {0: lambda a, b, c: a + b, 1: lambda a, b, c: a - b, 2: lambda a, b, c: -a, 3: lambda a, b, c: 2 * a,
+           4: lambda a, b, c: a + b - c, 5: lambda a, b, c: a + b + c, 6: lambda a, b, c: a - b - c,
+           7: lambda a, b, c: 3 * a - 2 * b, 8: lambda a, b, c: 3 * a + 2 * b}
+    for k in range(1, 9):
+        ops[8 + k] = (lambda kk: (lambda a, b, c: kk * a))(k)
+    n = 0
+    for i in range(900):
+        if i < len(edge) ** 2:
+            a, b = edge[i // len(edge)], edge[i % len(edge)]
+            c = edge[(i * 7) % len(edge)]
+        else:
+            a, b, c = rng.choice(vals), rng.choice(vals), rng.choice(vals)
+        for op, f in ops.items():
+            L.hc_fp_lc_raw(op, lim(a), lim(b), lim(c), out)
+            got = sum(int(out[j]) << (28 * j) for j in range(14))
+            assert all(int(out[j]) < (1 << 28) for j in range(14)), (op, a, b, c)
+            assert got == f(a, b, c) % q2, (op, hex(a), hex(b), hex(c))
+            n += 1
+    assert n == 900 * len(ops)
+
+
 def test_fp_legendre(L):
     """Binary-Jacobi Legendre symbol == Euler's criterion (squares, non-squares, 0, edges)."""
     rng = random.Random(21)
