@@ -20,6 +20,10 @@ BLS_INLINE fp_t f_dbl(const fp_t& a) { return fp_dbl(a); }
 BLS_INLINE fp2_t f_dbl(const fp2_t& a) { return fp2_dbl(a); }
 BLS_INLINE fp_t f_neg(const fp_t& a) { return fp_neg(a); }
 BLS_INLINE fp2_t f_neg(const fp2_t& a) { return fp2_neg(a); }
+BLS_INLINE fp_t f_sub2(const fp_t& a, const fp_t& b, const fp_t& c) { return fp_sub2(a, b, c); }
+BLS_INLINE fp2_t f_sub2(const fp2_t& a, const fp2_t& b, const fp2_t& c) { return fp2_sub2(a, b, c); }
+BLS_INLINE fp_t f_mul_small(const fp_t& a, int k) { return fp_mul_small(a, k); }
+BLS_INLINE fp2_t f_mul_small(const fp2_t& a, int k) { return fp2_mul_small(a, k); }
 BLS_INLINE bool f_is_zero(const fp_t& a) { return fp_is_zero(a); }
 BLS_INLINE bool f_is_zero(const fp2_t& a) { return fp2_is_zero(a); }
 BLS_INLINE bool f_eq(const fp_t& a, const fp_t& b) { return fp_eq(a, b); }
@@ -59,13 +63,12 @@ BLS_HD inline jac_t<F> jac_dbl(const jac_t<F>& p) {
   const F B = f_sqr(p.y);
   const F C = f_sqr(B);
   const F xb = f_add(p.x, B);
-  const F D = f_dbl(f_sub(f_sub(f_sqr(xb), A), C));
-  const F E = f_add(f_dbl(A), A);
+  const F D = f_dbl(f_sub2(f_sqr(xb), A, C));
+  const F E = f_mul_small(A, 3);
   const F Fv = f_sqr(E);
   jac_t<F> r;
-  r.x = f_sub(Fv, f_dbl(D));
-  const F c8 = f_dbl(f_dbl(f_dbl(C)));
-  r.y = f_sub(f_mul(E, f_sub(D, r.x)), c8);
+  r.x = f_sub2(Fv, D, D);
+  r.y = f_sub(f_mul(E, f_sub(D, r.x)), f_mul_small(C, 8));
   r.z = f_dbl(f_mul(p.y, p.z));
   return r;   // Z = 0 stays 0 (infinity doubles to infinity)
 }
@@ -91,7 +94,7 @@ BLS_HD inline jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
   const F HHH = f_mul(H, HH);
   const F V = f_mul(U1, HH);
   jac_t<F> r;
-  r.x = f_sub(f_sub(f_sqr(R), HHH), f_dbl(V));
+  r.x = f_sub2(f_sqr(R), HHH, f_dbl(V));
   r.y = f_sub(f_mul(R, f_sub(V, r.x)), f_mul(S1, HHH));
   r.z = f_mul(f_mul(p.z, q.z), H);
   return r;
@@ -114,7 +117,7 @@ BLS_HD inline jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
   const F HHH = f_mul(H, HH);
   const F V = f_mul(p.x, HH);
   jac_t<F> r;
-  r.x = f_sub(f_sub(f_sqr(R), HHH), f_dbl(V));
+  r.x = f_sub2(f_sqr(R), HHH, f_dbl(V));
   r.y = f_sub(f_mul(R, f_sub(V, r.x)), f_mul(p.y, HHH));
   r.z = f_mul(p.z, H);
   return r;

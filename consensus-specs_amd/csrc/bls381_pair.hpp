@@ -194,6 +194,8 @@ __device__ __forceinline__ fp2p_t f_mul(const fp2p_t& a, const fp2p_t& b) { retu
 __device__ __forceinline__ fp2p_t f_sqr(const fp2p_t& a) { return fp2_sqr(a); }
 __device__ __forceinline__ fp2p_t f_dbl(const fp2p_t& a) { return fp2_dbl(a); }
 __device__ __forceinline__ fp2p_t f_neg(const fp2p_t& a) { return fp2_neg(a); }
+__device__ __forceinline__ fp2p_t f_sub2(const fp2p_t& a, const fp2p_t& b, const fp2p_t& c) { return fp2_sub2(a, b, c); }
+__device__ __forceinline__ fp2p_t f_mul_small(const fp2p_t& a, int k) { return fp2_mul_small(a, k); }
 __device__ __forceinline__ bool f_is_zero(const fp2p_t& a) { return fp2_is_zero(a); }
 __device__ __forceinline__ bool f_eq(const fp2p_t& a, const fp2p_t& b) { return fp2_eq(a, b); }
 __device__ __forceinline__ fp2p_t f_inv(const fp2p_t& a) { return fp2_inv(a); }

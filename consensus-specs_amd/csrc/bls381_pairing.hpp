@@ -24,7 +24,7 @@ struct g1_line_pre {
 BLS_INLINE g1_line_pre g1_prepare(const aff_t<fp_t>& p) {
   g1_line_pre r;
   r.nx = fp_neg(p.x);
-  r.n3x = fp_add(fp_dbl(r.nx), r.nx);
+  r.n3x = fp_mul_small(r.nx, 3);
   r.y = p.y;
   r.y2 = fp_dbl(p.y);
   return r;
@@ -33,13 +33,6 @@ BLS_INLINE g1_line_pre g1_prepare(const aff_t<fp_t>& p) {
 // homogeneous-projective T on E'(Fp2)
 template <class E> struct g2_proj { E x, y, z; };
 
-template <class E>
-BLS_INLINE E fp2_mul_b(const E& a) {
-  // b' = 4(1+u): a * b' = 4 * xi * a
-  const E t = fp2_mul_xi(a);
-  return fp2_dbl(fp2_dbl(t));
-}
-
 // doubling step: T <- 2T, returns the tangent line at the old T evaluated at P
 template <class E>
 BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E& c2) {
@@ -47,9 +40,8 @@ BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E
   const E YY = fp2_sqr(T.y);
   const E ZZ = fp2_sqr(T.z);
   const E YZ = fp2_mul(T.y, T.z);
-  const E bZZ = fp2_mul_b(ZZ);
-  const E b3 = fp2_add(fp2_dbl(bZZ), bZZ);        // 3 b' Z^2
-  const E b9 = fp2_add(fp2_dbl(b3), b3);          // 9 b' Z^2
+  const E b3 = fp2_mul_small(fp2_mul_small(fp2_mul_xi(ZZ), 3), 4);   // 3 b' Z^2 = 12 xi Z^2
+  const E b9 = fp2_mul_small(b3, 3);                                 // 9 b' Z^2
   c0 = fp2_sub(YY, b3);
   c1 = fp2_mul_fp(XX, P.n3x);
   c2 = fp2_mul_fp(YZ, P.y2);
@@ -58,7 +50,7 @@ BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E
   const E b3sq = fp2_sqr(b3);                      // 9 b'^2 Z^4
   g2_proj<E> R;
   R.x = fp2_half(fp2_mul(XY, fp2_sub(YY, b9)));
-  R.y = fp2_sub(fp2_sqr(h), fp2_add(fp2_dbl(b3sq), b3sq));  // h^2 - 27 b'^2 Z^4
+  R.y = fp2_sub(fp2_sqr(h), fp2_mul_small(b3sq, 3));  // h^2 - 27 b'^2 Z^4
   R.z = fp2_dbl(fp2_mul(YY, YZ));
   T = R;
 }
@@ -74,7 +66,7 @@ BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre&
   const E vv = fp2_sqr(v);
   const E vvv = fp2_mul(vv, v);
   const E vvX = fp2_mul(vv, T.x);
-  const E A = fp2_sub(fp2_sub(fp2_mul(fp2_sqr(u), T.z), vvv), fp2_dbl(vvX));
+  const E A = fp2_sub2(fp2_mul(fp2_sqr(u), T.z), vvv, fp2_dbl(vvX));
   g2_proj<E> R;
   R.x = fp2_mul(v, A);
   R.y = fp2_sub(fp2_mul(u, fp2_sub(vvX, A)), fp2_mul(vvv, T.y));
@@ -118,20 +110,95 @@ BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P) {
   return miller_loop_n<1>(&Q, &P);
 }
 
-// f^|x| in the cyclotomic subgroup, then conjugate for x < 0.
-// |x| = 0xd201000000010000 has bits 63, 62, 60, 57, 48, 16: after r = f the
-// squarings come in runs of 1, 2, 3, 9, 32 (each followed by r *= f) and a
-// final 16.  One call per exponentiation; the runs are tight loops of inlined
-// cyclotomic squarings, so r stays in registers (only the five products pass
-// it through memory).
+// f^|x| in the cyclotomic subgroup by Granger-Scott squarings, then conjugate
+// for x < 0.  |x| = 0xd201000000010000 has bits 63, 62, 60, 57, 48, 16: after
+// r = f the squarings come in runs of 1, 2, 3, 9, 32 (each followed by r *= f)
+// and a final 16.  The runs are tight loops of inlined cyclotomic squarings, so
+// r stays in registers.  This is the exact fallback of cyc_exp_x below.
 BLS_CONST int CYC_X_RUNS[6] = {1, 2, 3, 9, 32, 16};
 
 template <class E>
-BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+BLS_NOINLINE fp12_g<E> cyc_exp_x_gs(const fp12_g<E>& f) {
   fp12_g<E> r = f;
   for (int s = 0; s < 6; ++s) {
     for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fp12_cyclotomic_sqr_inl(r);
     if (s < 5) r = fp12_mul(r, f);
+  }
+  return fp12_conj(r);
+}
+
+// Karabina compressed squaring.  With z = w^3, f = A + B w + C w^2 over
+// Fp4 = Fp2[z]; the Granger-Scott outputs B' = 3 z C^2 + 2 conj(B) and
+// C' = 3 B^2 - 2 conj(C) depend on B and C only, so
+//   (g2, g3, g4, g5) = (B0, B1, C0, C1) = (b0, a2, a1, b2)
+// squares on its own with six Fp2 squarings (Granger-Scott: nine), and
+// A = (a0, b1) comes back from the norm condition f conj(f) = 1:
+//   b1 = (xi g5^2 + 3 g4^2 - 2 g3) / (4 g2),  a0 = xi (2 b1^2 + g2 g5 - 3 g3 g4) + 1.
+// Mirrored by oracle/tower_model.py (cyc_csqr / cyc_decompress).
+template <class E> struct cyc_bc { E g2, g3, g4, g5; };
+
+template <class E>
+BLS_INLINE cyc_bc<E> cyc_compress(const fp12_g<E>& f) {
+  cyc_bc<E> g; g.g2 = f.c1.c0; g.g3 = f.c0.c2; g.g4 = f.c0.c1; g.g5 = f.c1.c2; return g;
+}
+
+template <class E>
+BLS_INLINE cyc_bc<E> cyc_csqr(const cyc_bc<E>& g) {
+  cyc_bc<E> r;
+  {
+    const E t0 = fp2_sqr(g.g4), t1 = fp2_sqr(g.g5), t2 = fp2_sqr(fp2_add(g.g4, g.g5));
+    r.g2 = fp2_3p2(fp2_mul_xi(fp2_sub2(t2, t0, t1)), g.g2);   // 6 xi g4 g5 + 2 g2
+    r.g3 = fp2_3m2(fp2_add_mul_xi(t0, t1), g.g3);             // 3 (g4^2 + xi g5^2) - 2 g3
+  }
+  const E t3 = fp2_sqr(g.g2), t4 = fp2_sqr(g.g3), t5 = fp2_sqr(fp2_add(g.g2, g.g3));
+  r.g4 = fp2_3m2(fp2_add_mul_xi(t3, t4), g.g4);               // 3 (g2^2 + xi g3^2) - 2 g4
+  r.g5 = fp2_3p2(fp2_sub2(t5, t3, t4), g.g5);                 // 6 g2 g3 + 2 g5
+  return r;
+}
+
+// the full element from (g2..g5) and 1 / (4 g2)
+template <class E>
+BLS_INLINE fp12_g<E> cyc_decompress(const cyc_bc<E>& g, const E& inv4g2) {
+  const E num = fp2_sub2(fp2_add_mul_xi(fp2_mul_small(fp2_sqr(g.g4), 3), fp2_sqr(g.g5)), g.g3, g.g3);
+  const E b1 = fp2_mul(num, inv4g2);
+  const E u = fp2_sub(fp2_add(fp2_dbl(fp2_sqr(b1)), fp2_mul(g.g2, g.g5)), fp2_mul_small(fp2_mul(g.g3, g.g4), 3));
+  fp12_g<E> f;
+  f.c0.c0 = fp2_add(fp2_mul_xi(u), e2_one<E>());
+  f.c0.c1 = g.g4; f.c0.c2 = g.g3;
+  f.c1.c0 = g.g2; f.c1.c1 = b1; f.c1.c2 = g.g5;
+  return f;
+}
+
+// f^x, right to left: f^|x| = prod over the six set bits b of f^(2^b).  The 63
+// squarings run compressed; the six snapshots share one Fp2 inversion
+// (Montgomery's trick) and are multiplied together.  A snapshot with g2 = 0 (f = 1,
+// or a point of measure zero) cannot be decompressed this way: if any lane of the
+// wave has one, the wave takes the Granger-Scott path instead (uniform branch).
+BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
+
+template <class E>
+BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+  cyc_bc<E> snap[6];
+  cyc_bc<E> g = cyc_compress(f);
+  bool zero = false;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cyc_csqr(g);
+    snap[s] = g;
+    const bool zs = fp2_is_zero(g.g2);   // evaluated on both lanes of a pair
+    zero = zero | zs;
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs(f);
+  // prefix products of the denominators 4 g2, one inversion, then back to front
+  E pre[6];
+  pre[0] = fp2_mul_small(snap[0].g2, 4);
+  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(snap[s].g2, 4));
+  E inv = fp2_inv(pre[5]);
+  fp12_g<E> r = fp12_one<E>();
+  for (int s = 5; s >= 0; --s) {
+    const E is = s ? fp2_mul(inv, pre[s - 1]) : inv;
+    if (s) inv = fp2_mul(inv, fp2_mul_small(snap[s].g2, 4));
+    const fp12_g<E> x = cyc_decompress(snap[s], is);
+    r = (s == 5) ? x : fp12_mul(r, x);
   }
   return fp12_conj(r);
 }

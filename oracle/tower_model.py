@@ -206,6 +206,47 @@ def cyc_exp_x(f):
     return conj12(cyc_exp_abs_x(f))   # x < 0
 
 
+# Karabina compressed squaring (bls381_pairing.hpp cyc_csqr / cyc_decompress / cyc_exp_x):
+# (g2, g3, g4, g5) = (b0, a2, a1, b2) squares on its own; (a0, b1) comes back from
+# the norm condition.
+def cyc_compress(f):
+    a0, a1, a2, b0, b1, b2 = f
+    return (b0, a2, a1, b2)
+
+
+def cyc_csqr(g):
+    g2, g3, g4, g5 = g
+    t0, t1, t2 = mul2(g4, g4), mul2(g5, g5), mul2(add2(g4, g5), add2(g4, g5))
+    t3, t4, t5 = mul2(g2, g2), mul2(g3, g3), mul2(add2(g2, g3), add2(g2, g3))
+    m = O.f2_muls
+    return (add2(m(mul_xi(sub2(sub2(t2, t0), t1)), 3), m(g2, 2)),
+            sub2(m(add2(t0, mul_xi(t1)), 3), m(g3, 2)),
+            sub2(m(add2(t3, mul_xi(t4)), 3), m(g4, 2)),
+            add2(m(sub2(sub2(t5, t3), t4), 3), m(g5, 2)))
+
+
+def cyc_decompress(g):
+    g2, g3, g4, g5 = g
+    m = O.f2_muls
+    num = sub2(add2(mul_xi(mul2(g5, g5)), m(mul2(g4, g4), 3)), m(g3, 2))
+    b1 = mul2(num, inv2(m(g2, 4)))
+    a0 = add2(mul_xi(sub2(add2(m(mul2(b1, b1), 2), mul2(g2, g5)), m(mul2(g3, g4), 3))), ONE2)
+    return (a0, g4, g3, g2, b1, g5)
+
+
+def cyc_exp_abs_x_compressed(f):
+    """f^|x| right to left: 63 compressed squarings, the six set bits' snapshots
+    decompressed and multiplied.  Requires every snapshot's g2 != 0."""
+    g = cyc_compress(f)
+    res = None
+    for run in (16, 32, 9, 3, 2, 1):
+        for _ in range(run):
+            g = cyc_csqr(g)
+        x = cyc_decompress(g)
+        res = x if res is None else mul12(res, x)
+    return res
+
+
 def final_exp(f):
     """Returns f^(3 (q^12-1)/r).  The factor 3 is coprime to r, so
     final_exp(f) == 1  <=>  f^((q^12-1)/r) == 1 (DESIGN.md "Final exponentiation").

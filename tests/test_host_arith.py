@@ -185,6 +185,12 @@ def test_fp12(L):
     L.hc_fp12_mul_by_line(b576(f), b96(c[0]), b96(c[1]), b96(c[2]), buf)
     assert i576(buf.raw) == M.mul12(f, (c[0], c[1], M.ZERO2, M.ZERO2, c[2], M.ZERO2))
     L.hc_final_exp(b576(f), buf); assert i576(buf.raw) == M.final_exp(f)
+    # f = 1 (the infinity/infinity verify): every compressed snapshot has g2 = 0, so the
+    # exponentiations by x take the exact Granger-Scott fallback
+    L.hc_final_exp(b576(M.ONE12), buf); assert i576(buf.raw) == M.ONE12
+    # an element of Fp6 (b = 0): the easy part maps it to 1 as well
+    g6 = f[:3] + (M.ZERO2,) * 3
+    L.hc_final_exp(b576(g6), buf); assert i576(buf.raw) == M.final_exp(g6) == M.ONE12
 
 
 def test_codecs_and_subgroups(L, golden):

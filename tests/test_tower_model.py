@@ -29,6 +29,21 @@ def test_cyclotomic_square_and_final_exp_chain():
     assert M.to_pyecc12(M.final_exp(f)) == O.f12_pow(M.to_pyecc12(f), 3 * (q ** 12 - 1) // O.r)
 
 
+def test_karabina_compressed_exponentiation():
+    """Compressed squarings of (g2..g5) track Granger-Scott squarings exactly, the
+    decompression recovers the full element, and f^|x| right to left equals the
+    square-and-multiply chain (bls381_pairing.hpp cyc_exp_x)."""
+    rng = random.Random(3)
+    f = tuple(_r2(rng) for _ in range(6))
+    t = M.mul12(M.conj12(f), M.inv12(f))
+    t = M.mul12(M.frob12(t, 2), t)
+    x, g = t, M.cyc_compress(t)
+    for _ in range(4):
+        x, g = M.cyclotomic_sqr(x), M.cyc_csqr(g)
+        assert M.cyc_compress(x) == g and M.cyc_decompress(g) == x
+    assert M.cyc_exp_abs_x_compressed(t) == M.cyc_exp_abs_x(t)
+
+
 def test_pairing_bilinear_and_relation_to_oracle():
     rng = random.Random(3)
     g1 = (O.g_x, O.g_y)
