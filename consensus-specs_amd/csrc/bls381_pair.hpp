@@ -36,7 +36,8 @@ enum : int {
 
 template <int CTRL>
 __device__ __forceinline__ uint32_t pr_dpp(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+  // mov_dpp: no old value to initialise (every lane of the quad is a valid source)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, false);
 }
 template <int CTRL>
 __device__ __forceinline__ fp_t pr_dpp(const fp_t& a) {
