@@ -21,6 +21,12 @@ constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 #ifndef BLS_WAVES_PER_EU
 #define BLS_WAVES_PER_EU 2
 #endif
+#ifndef BLS_ML_WAVES_PER_EU
+#define BLS_ML_WAVES_PER_EU BLS_WAVES_PER_EU
+#endif
+#ifndef BLS_FE_WAVES_PER_EU
+#define BLS_FE_WAVES_PER_EU BLS_WAVES_PER_EU
+#endif
 
 // ------------------------------------------------------------ SoA access --
 __device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
@@ -147,7 +153,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, 
 // --------------------------------------------------------- verify kernels --
 // One bls_verify per lane pair: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
 // infinity short-circuit of py_ecc's pairing (a pair with an infinite point is 1).
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
                                                          const uint8_t* __restrict__ sig_st,
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const uint8_t* __restrict__ pk_st,
@@ -180,7 +186,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_verify(size
   if (lead) st_out[i] = ST_OK;
 }
 
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {
   const size_t i = item_index<2>();
