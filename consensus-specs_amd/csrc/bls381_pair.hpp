@@ -97,10 +97,19 @@ __device__ __forceinline__ fp_t fp2p_sqr_body(const fp_t& a) {
   return fp_mul_body(x, y);
 }
 
-__device__ __attribute__((noinline)) fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
+// BLS_FP2_INLINE=1 inlines the Fp2 product bodies everywhere (experiment knob)
+#ifndef BLS_FP2_INLINE
+#define BLS_FP2_INLINE 0
+#endif
+#if BLS_FP2_INLINE
+#define BLS_FP2_CALL __device__ __forceinline__
+#else
+#define BLS_FP2_CALL __device__ __attribute__((noinline))
+#endif
+BLS_FP2_CALL fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
   return fp_pack(fp2p_mul_body(fp_unpack(a), fp_unpack(b)));
 }
-__device__ __attribute__((noinline)) fpv_t fp2p_sqr_call(fpv_t a) { return fp_pack(fp2p_sqr_body(fp_unpack(a))); }
+BLS_FP2_CALL fpv_t fp2p_sqr_call(fpv_t a) { return fp_pack(fp2p_sqr_body(fp_unpack(a))); }
 
 // ------------------------------------------------------------ Fp2 on a pair --
 __device__ __forceinline__ fp2p_t pr_make(const fp_t& v) { fp2p_t r; r.v = v; return r; }
