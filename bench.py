@@ -584,7 +584,9 @@ def main():
                 "macs_per_launch": launch_macs,
                 "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
                 "peak_source": peak_src}
-    whole = sum(counts.values()) * MACS_PER_FP_MUL * n / (1e-3 * sum(kern_ms.values())) / 1e12
+    # the whole pipeline's work over the timed step's wall time (kernels on the side stream overlap
+    # the main stream, so the sum of kernel times would double-count them)
+    whole = sum(counts.values()) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
     roofline["pipeline_achieved"] = round(whole, 3)
     roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
 

@@ -218,12 +218,12 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   std::lock_guard<std::mutex> lk(c->fork_mu);
   // decode_g1 (one lane per item: one wave per SIMD) and, by default, decode_g2
   // on the side stream, beside hash_to_g2; the Miller loop waits for both branches.
-  // The kernels use 128 VGPRs, so decode waves co-reside with the hash waves.
+  // Decode waves fill the SIMD slots that finished hash waves free (measured in DESIGN.md §10).
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
   LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
 #if BLS_DECODE_G2_SIDE
-  // both decodes behind hash_to_G2: their waves co-reside with the hash waves
+  // both decodes in sequence beside hash_to_G2
   LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
