@@ -599,16 +599,17 @@ BLS_HD inline fp_t fp_inv(const fp_t& am) {
     for (int i = 0; i < 12; ++i) { d[i] = sub_borrow(u[i], v[i], br, br); nz |= d[i]; }
     if (nz == 0) break;                 // u == v == gcd == 1
     // u > v: (u, x1) <- (u - v, x1 - x2);  u < v: (u, v, x1, x2) <- (v - u, u, x2 - x1, x1)
-    uint32_t xd[12], xn[12], nb = 0;
+    // x2 - x1 = 2q - xd: u != v here, so x1 != x2 (mod q) and xd lies in (0, 2q) \ {q}
+    uint32_t xd[12], nb = 0, xb = 0;
     words_sub_mod2q(xd, x1, x2);
-    words_sub_mod2q(xn, x2, x1);
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       const uint32_t nd = sub_borrow(0u, d[i], nb, nb);
+      const uint32_t xn = sub_borrow(Q2_WORDS[i], xd[i], xb, xb);
       const uint32_t uo = u[i], xo = x1[i];
       u[i] = br ? nd : d[i];
       v[i] = br ? uo : v[i];
-      x1[i] = br ? xn[i] : xd[i];
+      x1[i] = br ? xn : xd[i];
       x2[i] = br ? xo : x2[i];
     }
     xgcd_strip(u, x1);
