@@ -124,8 +124,9 @@ def load_pmc_traffic(prof_key, n):
     return None, None
 
 
-def count_fp_muls(pks, msgs, sigs, doms, k=8):
-    """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build."""
+def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
+    """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build
+    (strict = 1: with the subgroup checks of BLS381_POLICY_STRICT)."""
     import build_native
     path = build_native.build_hostcheck(count_ops=True)
     L = ctypes.CDLL(path)
@@ -134,7 +135,7 @@ def count_fp_muls(pks, msgs, sigs, doms, k=8):
     for i in range(64):
         out = (ctypes.c_uint64 * 5)()
         if L.hc_count_verify_stages(pks[48 * i:48 * i + 48], msgs[32 * i:32 * i + 32],
-                                    sigs[96 * i:96 * i + 96], doms[8 * i:8 * i + 8], out) == 1:
+                                    sigs[96 * i:96 * i + 96], doms[8 * i:8 * i + 8], strict, out) == 1:
             tot += np.array(list(out), dtype=float)
             done += 1
             if done == k:

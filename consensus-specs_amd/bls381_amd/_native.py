@@ -19,7 +19,8 @@ EINVAL_POINT = -1
 EARG = -2
 ENODEV = -3
 EHIP = -4
-MSG_MAX = 256
+MSG_MAX = 1 << 20           # BLS381_MSG_MAX
+POLICY = {"pyecc": 0, "strict": 1}   # BLS381_POLICY_PYECC / _STRICT
 
 # every symbol include/bls381.h declares, with its ctypes signature
 _u8p = ctypes.c_void_p
@@ -28,6 +29,8 @@ _SIGS = {
     "bls381_init": (ctypes.c_int, [ctypes.c_int]),
     "bls381_shutdown": (None, []),
     "bls381_last_error": (ctypes.c_char_p, []),
+    "bls381_set_subgroup_policy": (ctypes.c_int, [ctypes.c_int]),
+    "bls381_get_subgroup_policy": (ctypes.c_int, []),
     "bls381_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "bls381_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "bls381_verify": (ctypes.c_int, [_u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]),
@@ -136,6 +139,18 @@ def _buf(b: bytes):
 
 def init(device: int = 0) -> None:
     check(lib().bls381_init(device))
+
+
+def set_subgroup_policy(name: str) -> None:
+    """'pyecc' or 'strict' (include/bls381.h BLS381_POLICY_*); process-wide."""
+    if name not in POLICY:
+        raise ValueError("unknown subgroup policy %r (expected one of %s)" % (name, sorted(POLICY)))
+    check(load_library().bls381_set_subgroup_policy(POLICY[name]))
+
+
+def get_subgroup_policy() -> str:
+    code = load_library().bls381_get_subgroup_policy()
+    return {v: k for k, v in POLICY.items()}[code]
 
 
 def verify(pk: bytes, msg: bytes, sig: bytes, dom8: bytes) -> bool:

@@ -11,6 +11,18 @@ the same error behaviour as the py_ecc 1.7.0 calls they replace
 * bls_verify_multiple raises ValidationError (a ValueError) on a length mismatch;
 * bls_aggregate_* raise ValueError on an invalid point encoding;
 * a domain outside [0, 2^64) raises OverflowError (int.to_bytes).
+
+Messages may have any length up to _native.MSG_MAX (1 MiB; the spec's
+message_hash is Bytes32), and one bls_verify_multiple call may mix lengths (each
+length group becomes a partial Miller product; one final exponentiation decides
+the call).  A longer message raises ValueError instead of returning a verdict.
+
+Two switches mirror behaviour the reference leaves to py_ecc:
+* DOMAIN_BYTEORDER -- how the int domain becomes 8 bytes (SURVEY.md A.2);
+* SUBGROUP_POLICY  -- "pyecc" (default): py_ecc 1.7.0's checks, decoding and
+  on-curve only; "strict": every pubkey / signature must also lie in G1 / G2
+  (specs/bls_signature.md:135-136,143-144).  The verdicts differ only on points
+  with a small-order component (tests/golden/bls_torsion.json has both columns).
 """
 from . import _native
 
@@ -23,6 +35,10 @@ STUB_PUBKEY = b'\x22' * 48
 
 # py_ecc 1.7.0 serialises the int domain big-endian; one switch.
 DOMAIN_BYTEORDER = "big"
+
+# Subgroup checks on the verify paths: "pyecc" (py_ecc 1.7.0, the reference's
+# behaviour) or "strict" (the spec's valid-G1/G2-point rule).  One switch.
+SUBGROUP_POLICY = "pyecc"
 
 
 class ValidationError(ValueError):
@@ -59,12 +75,20 @@ def _sk32(privkey) -> bytes:
     return k.to_bytes(32, "big")
 
 
+def _check_len(message_hash: bytes) -> None:
+    if len(message_hash) > _native.MSG_MAX:
+        raise ValueError("message of %d bytes is longer than the engine's %d-byte limit"
+                         % (len(message_hash), _native.MSG_MAX))
+
+
 @only_with_bls(alt_return=True)
 def bls_verify(pubkey, message_hash, signature, domain):
     dom8 = _dom8(domain)
     pubkey, message_hash, signature = bytes(pubkey), bytes(message_hash), bytes(signature)
-    if len(pubkey) != 48 or len(signature) != 96 or len(message_hash) > _native.MSG_MAX:
+    _check_len(message_hash)
+    if len(pubkey) != 48 or len(signature) != 96:
         return False
+    _native.set_subgroup_policy(SUBGROUP_POLICY)
     return _native.verify(pubkey, message_hash, signature, dom8)
 
 
@@ -77,13 +101,32 @@ def bls_verify_multiple(pubkeys, message_hashes, signature, domain):
     pks = [bytes(p) for p in pubkeys]
     msgs = [bytes(m) for m in message_hashes]
     signature = bytes(signature)
+    for m in msgs:
+        _check_len(m)
     if any(len(p) != 48 for p in pks) or len(signature) != 96:
         return False
-    lens = {len(m) for m in msgs}
-    if len(lens) > 1 or (lens and max(lens) > _native.MSG_MAX):
-        return False  # mixed-length messages are outside the engine's batch layout
-    mlen = lens.pop() if lens else 32
-    return _native.verify_multiple(b"".join(pks), b"".join(msgs), mlen, signature, dom8)
+    _native.set_subgroup_policy(SUBGROUP_POLICY)
+    return verify_multiple_bytes(pks, msgs, signature, dom8)
+
+
+def verify_multiple_bytes(pks, msgs, signature: bytes, dom8: bytes) -> bool:
+    """bls_verify_multiple on validated bytes (48-byte keys, 96-byte signature, messages
+    of any lengths <= MSG_MAX) under the policy already set."""
+    lens = sorted({len(m) for m in msgs})
+    if len(lens) <= 1:
+        mlen = lens[0] if lens else 32
+        return _native.verify_multiple(b"".join(pks), b"".join(msgs), mlen, signature, dom8)
+    # mixed lengths: one partial Miller product per length (the signature pair in
+    # the first), multiplied and finally exponentiated once -- py_ecc's product
+    parts = []
+    for j, mlen in enumerate(lens):
+        sel = [i for i, m in enumerate(msgs) if len(m) == mlen]
+        rc, part = _native.miller_partial(b"".join(pks[i] for i in sel), b"".join(msgs[i] for i in sel), mlen,
+                                          signature, j == 0, dom8)
+        if rc != 0:
+            return False
+        parts.append(part)
+    return _native.final_verify(b"".join(parts))
 
 
 # Optional device-resident pubkey registry (registry.PubkeyRegistry): when set,
@@ -119,8 +162,7 @@ def bls_aggregate_signatures(signatures):
 @only_with_bls(alt_return=STUB_SIGNATURE)
 def bls_sign(message_hash, privkey, domain):
     message_hash = bytes(message_hash)
-    if len(message_hash) > _native.MSG_MAX:
-        raise ValueError("message longer than the engine's limit")
+    _check_len(message_hash)
     return _native.sign(message_hash, _sk32(privkey), _dom8(domain))
 
 

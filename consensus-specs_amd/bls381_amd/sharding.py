@@ -29,6 +29,7 @@ from __future__ import annotations
 from typing import Callable, List, Optional, Sequence
 
 PART_BYTES = 576
+MSG_MAX = 1 << 20   # BLS381_MSG_MAX
 
 
 class ValidationError(ValueError):
@@ -70,16 +71,27 @@ def sharded_verify_multiple(pubkeys, message_hashes, signature, domain, *, rank:
     dom8 = int(domain).to_bytes(8, byteorder)
     msgs = [bytes(m) for m in message_hashes]
     pks = [bytes(p) for p in pubkeys]
-    mlen = len(msgs[0]) if msgs else 32
-    bad_shape = any(len(p) != 48 for p in pks) or len(bytes(signature)) != 96 or any(len(m) != mlen for m in msgs)
+    if any(len(m) > MSG_MAX for m in msgs):
+        raise ValueError("message longer than the engine's %d-byte limit" % MSG_MAX)
+    bad_shape = any(len(p) != 48 for p in pks) or len(bytes(signature)) != 96
     mine = partition_messages(msgs, world)[rank]
-    if bad_shape:
-        st, part = 1, bytes(PART_BYTES)
-    else:
-        st, part = partial_fn(b"".join(pks[i] for i in mine), b"".join(msgs[i] for i in mine), mlen,
-                              bytes(signature), rank == 0, dom8)
+    # one partial per distinct message length (the batch ABI takes one length
+    # per launch); every rank sends one per length of the whole call, so the
+    # all-gathered payloads have equal sizes.  The signature pair rides in rank
+    # 0's first partial.
+    lens = sorted({len(m) for m in msgs}) or [32]
+    st, parts = 0, []
+    for j, mlen in enumerate(lens):
+        sel = [i for i in mine if len(msgs[i]) == mlen]
+        if bad_shape:
+            s, part = 1, bytes(PART_BYTES)
+        else:
+            s, part = partial_fn(b"".join(pks[i] for i in sel), b"".join(msgs[i] for i in sel), mlen,
+                                 bytes(signature), rank == 0 and j == 0, dom8)
+        st |= 1 if s else 0
+        parts.append(part)
     dev = device if device is not None else torch.device("cpu")
-    payload = torch.tensor(list(bytes([1 if st else 0]) + part), dtype=torch.uint8, device=dev)
+    payload = torch.tensor(list(bytes([st]) + b"".join(parts)), dtype=torch.uint8, device=dev)
     gathered = [torch.empty_like(payload) for _ in range(world)]
     dist.all_gather(gathered, payload, group=group)
     verdict = torch.zeros(1, dtype=torch.uint8, device=dev)
@@ -146,8 +158,14 @@ def _native_batch(call_off, pks: bytes, msgs: bytes, mlen: int, sigs: bytes, dom
     return [bool(v) for v in _native.verify_multiple_batch(call_off, pks, msgs, mlen, sigs, dom8s)]
 
 
+def _native_mixed(pks, msgs, sig: bytes, dom8: bytes) -> bool:
+    from . import bls
+    return bls.verify_multiple_bytes(pks, msgs, sig, dom8)
+
+
 def sharded_verify_multiple_batch(calls, *, rank: int, world: int, group=None, device=None,
-                                  batch_fn: Optional[Callable] = None, byteorder: str = "big") -> List[bool]:
+                                  batch_fn: Optional[Callable] = None, mixed_fn: Optional[Callable] = None,
+                                  byteorder: str = "big") -> List[bool]:
     """Independent calls (pubkeys, message_hashes, signature, domain), contiguous ranges per rank.
 
     Every rank passes the same call list and gets every verdict back.  A call
@@ -163,14 +181,22 @@ def sharded_verify_multiple_batch(calls, *, rank: int, world: int, group=None, d
     dev = device if device is not None else torch.device("cpu")
     lo, hi = shard_range(len(calls), rank, world)
     mine = calls[lo:hi]
+    for _, msgs, _, _ in calls:
+        if any(len(bytes(m)) > MSG_MAX for m in msgs):
+            raise ValueError("message longer than the engine's %d-byte limit" % MSG_MAX)
     # the batch ABI takes one message length per launch: bucket calls by it;
-    # bad sizes / mixed lengths in one call -> False, as bls.bls_verify_multiple
+    # bad sizes -> False, as bls.bls_verify_multiple; a call mixing message
+    # lengths goes through mixed_fn (per-length partial products, one FE)
+    mixed_fn = mixed_fn or _native_mixed
     verdicts = [False] * len(mine)
     buckets = {}
-    for j, (pks, msgs, s, _) in enumerate(mine):
+    for j, (pks, msgs, s, d) in enumerate(mine):
+        if any(len(bytes(p)) != 48 for p in pks) or len(bytes(s)) != 96:
+            continue
         lens = {len(bytes(m)) for m in msgs}
-        if len(lens) > 1 or (lens and max(lens) > 256) or any(len(bytes(p)) != 48 for p in pks) \
-                or len(bytes(s)) != 96:
+        if len(lens) > 1:
+            verdicts[j] = bool(mixed_fn([bytes(p) for p in pks], [bytes(m) for m in msgs], bytes(s),
+                                        int(d).to_bytes(8, byteorder)))
             continue
         buckets.setdefault(lens.pop() if lens else 32, []).append(j)
     for mlen, idx in buckets.items():

@@ -43,18 +43,26 @@ def build_hip(force=False, extra=()):
     return out
 
 
+# the ASan/UBSan host build (~60 MB) is a CPU-test artefact: it lives outside the tree,
+# so it never rides along to the GPU box
+SANITIZE_DIR = os.environ.get("BLS381_SANITIZE_DIR", os.path.expanduser("~/.cache/bls381_amd"))
+
+
 def build_hostcheck(force=False, sanitize=False, count_ops=False):
     os.makedirs(LIB, exist_ok=True)
     name = "libbls381_hostcheck_asan.so" if sanitize else (
         "libbls381_hostcheck_count.so" if count_ops else "libbls381_hostcheck.so")
-    out = os.path.join(LIB, name)
+    if sanitize:
+        os.makedirs(SANITIZE_DIR, exist_ok=True)
+    out = os.path.join(SANITIZE_DIR if sanitize else LIB, name)
     src = os.path.join(CSRC, "host_check.cpp")
     deps = [src] + [os.path.join(CSRC, f) for f in HEADERS if f != "bls381_kernels.hpp"]
     if not force and _newer(out, deps):
         return out
-    cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas", "-I", CSRC, src, "-o", out]
+    cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-pthread", "-Wall", "-Wno-unknown-pragmas", "-I", CSRC, src, "-o", out]
     if sanitize:
-        cmd[3:3] = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-g"]
+        # -O0: the sanitized build of these fully unrolled headers takes ~10 min at -O2 -g
+        cmd[2:3] = ["-O0", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     if count_ops:
         cmd[3:3] = ["-DBLS_COUNT_OPS"]
     _run(cmd)

@@ -6,6 +6,7 @@
 // returns BLS381_ENODEV.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -27,6 +28,11 @@ namespace {
 
 thread_local std::string t_err;
 thread_local int t_device = -1;
+
+// Subgroup policy of the verify paths (bls381_set_subgroup_policy); read when a
+// pipeline is queued.  Default: py_ecc 1.7.0's behaviour.
+std::atomic<int> g_policy{BLS381_POLICY_PYECC};
+int check_subgroups() { return g_policy.load(std::memory_order_relaxed) == BLS381_POLICY_STRICT ? 1 : 0; }
 
 // Host memory that an async copy still reads: released once an event
 // recorded after the copy has completed (device-pointer entry points return
@@ -215,20 +221,21 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
                      const uint8_t* doms, uint8_t* verdicts, void* ws, hipStream_t s) {
   VerifyWs w = carve_verify(ws, n);
   const dim3 g(grid_for(n)), g2(grid_for(2 * n)), b(KBLOCK);   // G1: lane per item; G2/Fp12: lane pair
+  const int chk = check_subgroups();
   std::lock_guard<std::mutex> lk(c->fork_mu);
   // decode_g1 (one lane per item: one wave per SIMD) and, by default, decode_g2
   // on the side stream, beside hash_to_g2; the Miller loop waits for both branches.
   // Decode waves fill the SIMD slots that finished hash waves free (measured in DESIGN.md §10).
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, 1);
+  LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
 #if BLS_DECODE_G2_SIDE
   // both decodes in sequence beside hash_to_G2
-  LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
+  LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk);
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
   HIPC(hipEventRecord(c->ev_join, c->side));
-  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, 1);
+  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk);
 #endif
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
@@ -286,7 +293,7 @@ size_t agg_ws_size(const AggPlan& p, int ncomp) {
 template <class F>
 int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStream_t s,
             const uint32_t** out_jac, const uint8_t** out_bad, size_t* used, size_t cap = SIZE_MAX,
-            const agg_reg_src* reg = nullptr) {
+            const agg_reg_src* reg = nullptr, int check = 0) {
   Bump b(ws, cap);
   const uint32_t* prev_jac = nullptr;
   const uint8_t* prev_bad = nullptr;
@@ -303,18 +310,18 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
     const bool lanes = std::is_same<F, fp_t>::value && l == 0 && n_in_total < AGG_LANE_AVG_MAX * lv.size();
     if (lanes) {
       LAUNCH("agg_lane_sum", s, dim3(grid_for(lv.size())), dim3(KBLOCK), k_agg_lanes<AGG_REGISTRY>, (size_t)lv.size(),
-             (const agg_chunk*)d_chunks, d_in, jac, bad, reg ? *reg : none);
+             (const agg_chunk*)d_chunks, d_in, jac, bad, reg ? *reg : none, check);
     } else if (l == 0 && reg) {
       LAUNCH("agg_registry_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_REGISTRY>),
              (size_t)lv.size(), (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0,
-             (const uint8_t*)nullptr, jac, bad, *reg);
+             (const uint8_t*)nullptr, jac, bad, *reg, check);
     } else if (l == 0) {
       LAUNCH("agg_decode_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_BYTES>), (size_t)lv.size(),
              (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0, (const uint8_t*)nullptr, jac, bad,
-             none);
+             none, check);
     } else {
       LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_JAC>), (size_t)lv.size(),
-             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad, none);
+             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad, none, 0);
     }
     prev_jac = jac;
     prev_bad = bad;
@@ -434,8 +441,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_pairs_batch
   }
   fp12p_t f = fp12_one<fp2p_t>();
   uint8_t st = ST_OK;
-  if (sq == ST_BAD || sp == ST_BAD) st = ST_BAD;
-  else if (sq == ST_OK && sp == ST_OK) f = miller_loop_1(Q, g1_prepare(P));
+  if (sq == ST_BAD || sp == ST_BAD) {
+    st = ST_BAD;
+  } else if (sq == ST_OK && sp == ST_OK) {
+    bool degen = false;
+    f = miller_loop_1(Q, g1_prepare(P), degen);
+    if (degen) st = ST_BAD;   // py_ecc's zero pairing value (miller_loop_n)
+  }
   soa_st12(f_out, npairs, k, f);
   if (!pr_odd()) st_out[k] = st;
 }
@@ -484,6 +496,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bum
   uint8_t* h_st = b.take<uint8_t>(G + 1);
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
+  const int chk = check_subgroups();   // STRICT: every member key and signature is checked
   {
     std::lock_guard<std::mutex> fk(c->fork_mu);
     hipStream_t side = c->side;
@@ -495,13 +508,13 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bum
       const uint8_t* bad;
       size_t used = 0;
       uint8_t* sub = b.take<uint8_t>(0);
-      int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, side, &jac, &bad, &used, b.left());
+      int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, side, &jac, &bad, &used, b.left(), nullptr, chk);
       if (rc) return rc;
       b.off += used;
       LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
     }
     LAUNCH("decode_g2", side, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs,
-           sig_aff, sig_st, 1);
+           sig_aff, sig_st, chk);
     HIPC(hipEventRecord(c->ev_join, side));
     if (G > 0)
       LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs,
@@ -589,6 +602,14 @@ void bls381_shutdown(void) {
 }
 
 const char* bls381_last_error(void) { return t_err.c_str(); }
+
+int bls381_set_subgroup_policy(int policy) {
+  if (policy != BLS381_POLICY_PYECC && policy != BLS381_POLICY_STRICT) return BLS381_EARG;
+  g_policy.store(policy, std::memory_order_relaxed);
+  return 0;
+}
+
+int bls381_get_subgroup_policy(void) { return g_policy.load(std::memory_order_relaxed); }
 
 int bls381_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -790,7 +811,11 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) try {
 
 // ---- aggregation
 static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets, size_t n_pts, const uint8_t* d_pts,
-                          uint8_t* d_out, int32_t* d_status, void* ws, hipStream_t s) {
+                          uint8_t* d_out, int32_t* d_status, void* ws, size_t ws_cap, hipStream_t s) {
+  // the offsets must describe exactly the n_pts points given, in order
+  if (offsets[0] != 0 || offsets[ng] != n_pts) { t_err = "offsets disagree with n_pks"; return BLS381_EARG; }
+  for (size_t g = 0; g < ng; ++g)
+    if (offsets[g + 1] < offsets[g]) { t_err = "offsets not monotone"; return BLS381_EARG; }
   // the chunk lists are async-copy sources: they live until the stream passes them
   auto hold = std::make_shared<AggPlan>(plan_agg(ng, offsets));
   const AggPlan& plan = *hold;
@@ -798,12 +823,11 @@ static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets,
   const uint8_t* bad;
   size_t used = 0;
   int rc;
-  (void)n_pts;
   if (is_g2) {
-    if ((rc = run_agg<fp2p_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
+    if ((rc = run_agg<fp2p_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(2 * ng)), dim3(KBLOCK), k_agg_compress<fp2p_t>, ng, jac, bad, d_out, d_status);
   } else {
-    if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used))) return rc;
+    if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
   }
   return keep_until_done(c, s, hold);
@@ -822,17 +846,22 @@ size_t bls381_aggregate_pubkeys_batch_workspace_size(size_t n_groups, size_t n_p
 
 int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_offsets, size_t n_pks,
                                           const uint8_t* d_pks, uint8_t* d_out48, int32_t* d_status,
-                                          void* d_workspace, void* stream) {
+                                          void* d_workspace, void* stream) try {
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   if (n_groups == 0) return 0;
-  if (!h_offsets || !d_out48 || !d_status || !d_workspace) return BLS381_EARG;
+  if (!h_offsets || !d_out48 || !d_status || !d_workspace || (n_pks && !d_pks)) return BLS381_EARG;
   hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream (torch's default stream)
-  return agg_batch_impl(c, 0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace, s);
+  return agg_batch_impl(c, 0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace,
+                        bls381_aggregate_pubkeys_batch_workspace_size(n_groups, n_pks), s);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
-static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t* pts, uint8_t* out, int32_t* status) {
+static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t* pts, uint8_t* out,
+                    int32_t* status) try {
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
@@ -847,11 +876,16 @@ static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t
   int32_t* d_st = b.take<int32_t>(ng);
   hipStream_t s = c->stream;
   if (npts) HIPC(hipMemcpyAsync(d_pts, pts, npts * bytes, hipMemcpyHostToDevice, s));
-  if ((rc = agg_batch_impl(c, is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off), s))) return rc;
+  if ((rc = agg_batch_impl(c, is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off),
+                           b.left() > 256 ? b.left() - 256 : 0, s)))
+    return rc;
   HIPC(hipMemcpyAsync(out, d_out, ng * bytes, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(status, d_st, ng * 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
 }
 
 int bls381_aggregate_pubkeys_batch(size_t n_groups, const uint32_t* offsets, const uint8_t* pks, uint8_t* out48,

@@ -65,6 +65,38 @@ BLS_HD inline void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
   for (int i = 0; i < 8; ++i) out[i] = h[i];
 }
 
+// SHA-256 of msg || dom8 || tag (mlen + 9 bytes), the input of hash_to_G2's two
+// coordinate hashes (bls_signature.md:76-77), read straight from msg: no copy,
+// no per-lane buffer, so the message may be any length.
+BLS_HD inline void sha256_msg_dom_tag(uint32_t out[8], const uint8_t* msg, uint32_t mlen, const uint8_t dom8[8],
+                                      uint8_t tag) {
+  uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                   0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  const uint64_t len = (uint64_t)mlen + 9;
+  const uint64_t bitlen = len * 8;
+  const uint64_t nblocks = (len + 9 + 63) / 64;
+  for (uint64_t bi = 0; bi < nblocks; ++bi) {
+    uint32_t blk[16];
+    for (int wi = 0; wi < 16; ++wi) {
+      uint32_t word = 0;
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t pos = bi * 64 + wi * 4 + k;
+        uint8_t byte;
+        if (pos < mlen) byte = msg[pos];
+        else if (pos < (uint64_t)mlen + 8) byte = dom8[pos - mlen];
+        else if (pos == (uint64_t)mlen + 8) byte = tag;
+        else if (pos == len) byte = 0x80;
+        else if (pos >= nblocks * 64 - 8) byte = (uint8_t)(bitlen >> (8 * (nblocks * 64 - 1 - pos)));
+        else byte = 0;
+        word = (word << 8) | byte;
+      }
+      blk[wi] = word;
+    }
+    sha256_compress(h, blk);
+  }
+  for (int i = 0; i < 8; ++i) out[i] = h[i];
+}
+
 // 8 big-endian digest words -> plain Fp limbs (256-bit value < q)
 BLS_INLINE fp_t fp_plain_from_digest(const uint32_t d[8]) {
   uint8_t b[48];
@@ -86,16 +118,12 @@ BLS_INLINE E g2_select_root(const E& y) {
 // try-and-increment part of hash_to_G2 (bls_signature.md:74-86), before the cofactor.
 // msg may be any length (py_ecc hashes any bytes); dom8 = 8 domain bytes.
 BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, uint32_t mlen,
-                                       const uint8_t dom8[8], uint8_t* scratch /* mlen + 9 */) {
-  for (uint32_t i = 0; i < mlen; ++i) scratch[i] = msg[i];
-  for (int i = 0; i < 8; ++i) scratch[mlen + i] = dom8[i];
+                                       const uint8_t dom8[8]) {
   uint32_t d[8];
-  scratch[mlen + 8] = 1;
-  sha256(d, scratch, mlen + 9);
+  sha256_msg_dom_tag(d, msg, mlen, dom8, 1);
   fp2_t x;
   x.c0 = fp_to_mont(fp_plain_from_digest(d));
-  scratch[mlen + 8] = 2;
-  sha256(d, scratch, mlen + 9);
+  sha256_msg_dom_tag(d, msg, mlen, dom8, 2);
   x.c1 = fp_to_mont(fp_plain_from_digest(d));
   // rhs is a square in Fp2 iff its norm is a square in Fp: the cheap Legendre
   // test finds the candidate, then one square root is taken
@@ -172,9 +200,8 @@ BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
 
 // full hash_to_G2 for a 32-byte message; returns false only if the result is infinity
 BLS_HD inline bool hash_to_g2_aff(aff_t<fp2_t>& out, const uint8_t msg[32], const uint8_t dom8[8]) {
-  uint8_t scratch[41];
   aff_t<fp2_t> c;
-  hash_to_g2_candidate(c, msg, 32, dom8, scratch);
+  hash_to_g2_candidate(c, msg, 32, dom8);
   return jac_to_aff(out, g2_mul_cofactor(c));
 }
 

@@ -14,6 +14,14 @@ namespace bls381 {
 
 enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2 };
 
+// Subgroup policy (include/bls381.h BLS381_POLICY_*; DESIGN.md "Subgroup policy").
+//   PYECC:  py_ecc 1.7.0's checks only -- on-curve decoding, no subgroup test; the
+//           reduced pairing then ignores torsion of order prime to r in a pubkey,
+//           and a degenerate Miller loop (miller_loop_n) yields verdict False.
+//   STRICT: every pubkey and signature must lie in G1 / G2
+//           (specs/bls_signature.md:135-136,143-144).  Aggregates never check.
+// The kernels take the policy as a `check` / `check_subgroup` flag.
+
 constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 // minimum waves per SIMD requested from the register allocator for the heavy
 // per-item kernels (1 = up to 512 VGPR+AGPR per lane, 2 = up to 256).  Two:
@@ -139,11 +147,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, 
                                                    uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
   const size_t i = item_index<2>();
   if (i >= n) return;
-  uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
   aff_t<fp2p_t> c;
-  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   aff_t<fp2p_t> h;
   const bool fin = jac_to_aff(h, g2_mul_cofactor(c));
   if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
@@ -179,11 +186,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(s
     ++np;
   }
   fp12p_t f;
-  if (np == 2) f = miller_loop_n<2>(Q, P);
-  else if (np == 1) f = miller_loop_n<1>(Q, P);
+  bool degen = false;
+  if (np == 2) f = miller_loop_n<2>(Q, P, degen);
+  else if (np == 1) f = miller_loop_n<1>(Q, P, degen);
   else f = fp12_one<fp2p_t>();
   soa_st12(f_out, n, i, f);
-  if (lead) st_out[i] = ST_OK;
+  // a degenerate loop is py_ecc's zero pairing value: verdict False
+  if (lead) st_out[i] = degen ? ST_BAD : ST_OK;
 }
 
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
@@ -210,10 +219,12 @@ template <class F> struct pt_traits;
 template <> struct pt_traits<fp_t> {
   static constexpr int BYTES = 48;
   __device__ static int decode(aff_t<fp_t>& a, const uint8_t* b) { return g1_decompress(a, b); }
+  __device__ static bool in_subgroup(const aff_t<fp_t>& a) { return g1_in_subgroup(a); }
 };
 template <> struct pt_traits<fp2p_t> {
   static constexpr int BYTES = 96;
   __device__ static int decode(aff_t<fp2p_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
+  __device__ static bool in_subgroup(const aff_t<fp2p_t>& a) { return g2_in_subgroup(a); }
 };
 
 template <class F> __device__ aff_t<F> reg_ld_aff(const uint32_t* aff, size_t cap, size_t r);
@@ -236,22 +247,29 @@ struct agg_reg_src {
   size_t size;            // entries in use: an entry >= size is an error (BAD), never read
 };
 
-// adds level-1 input e (compressed bytes, or a registry entry) to acc
+// adds level-1 input e (compressed bytes, or a registry entry) to acc; with
+// `check` (STRICT policy, verify_multiple) a point outside the subgroup is bad
 template <class F, int MODE>
 __device__ __forceinline__ void agg_accumulate(jac_t<F>& acc, bool& bad, uint32_t e, const uint8_t* in_bytes,
-                                               const agg_reg_src& reg) {
+                                               const agg_reg_src& reg, int check) {
   if (MODE == AGG_REGISTRY) {
     const int32_t r = reg.entry ? reg.entry[e] : -1;
     if ((r >= 0 && (size_t)r >= reg.size) || (r < 0 && !in_bytes)) { bad = true; return; }
     if (r >= 0) {
       const uint8_t rs = reg.st[r];
-      if (rs == ST_BAD) bad = true;
-      else if (rs == ST_OK) acc = jac_add_aff(acc, reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r));
+      if (rs == ST_BAD) {
+        bad = true;
+      } else if (rs == ST_OK) {
+        const aff_t<F> a = reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r);
+        if (check && !pt_traits<F>::in_subgroup(a)) bad = true;
+        else acc = jac_add_aff(acc, a);
+      }
       return;
     }
   }
   aff_t<F> a;
-  const int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
+  int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
+  if (s == PT_OK && check && !pt_traits<F>::in_subgroup(a)) s = PT_BAD;
   if (s == PT_BAD) bad = true;
   else if (s == PT_OK) acc = jac_add_aff(acc, a);
 }
@@ -263,13 +281,13 @@ template <int MODE>
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_lanes(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                      const uint8_t* __restrict__ in_bytes,
                                                      uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad,
-                                                     agg_reg_src reg) {
+                                                     agg_reg_src reg, int check) {
   const size_t c = item_index<1>();
   if (c >= nchunks) return;
   const agg_chunk ch = chunks[c];
   jac_t<fp_t> acc = jac_infinity<fp_t>();
   bool bad = false;
-  for (uint32_t e = ch.begin; e < ch.end; ++e) agg_accumulate<fp_t, MODE>(acc, bad, e, in_bytes, reg);
+  for (uint32_t e = ch.begin; e < ch.end; ++e) agg_accumulate<fp_t, MODE>(acc, bad, e, in_bytes, reg, check);
   soa_jac<fp_t>::st(out_jac, nchunks, c, acc);
   out_bad[c] = bad ? 1 : 0;
 }
@@ -280,7 +298,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t 
                                                       const uint32_t* __restrict__ in_jac, size_t n_in,
                                                       const uint8_t* __restrict__ in_bad,
                                                       uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad,
-                                                      agg_reg_src reg) {
+                                                      agg_reg_src reg, int check) {
   constexpr int LPI = lanes_per<F>::N;
   constexpr int NW = sizeof(jac_t<F>) / 4;   // words per lane
   __shared__ uint32_t lds[KBLOCK * NW];
@@ -299,7 +317,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t 
       acc = jac_add(acc, soa_jac<F>::ld(in_jac, n_in, e));
       continue;
     }
-    agg_accumulate<F, MODE>(acc, bad, e, in_bytes, reg);
+    agg_accumulate<F, MODE>(acc, bad, e, in_bytes, reg, check);
   }
   if (bad) bad_any = 1;
   // tree reduction through LDS (lane-major words: conflict-free stride-1 access);
@@ -344,7 +362,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_compress(size_
   if (lead) status[g] = 0;
 }
 
-// per group: Jacobian G1 sum -> affine + status (OK / INF / BAD incl. subgroup)
+// per group: Jacobian G1 sum -> affine + status (OK / INF / BAD).  The members'
+// subgroup checks (STRICT policy) ran when they were decoded; py_ecc checks none.
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g1_affine(size_t ng, const uint32_t* __restrict__ jac,
                                                          const uint8_t* __restrict__ bad,
                                                          uint32_t* __restrict__ out_aff, uint8_t* __restrict__ st) {
@@ -353,7 +372,6 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g1_affine(size
   if (bad[g]) { st[g] = ST_BAD; return; }
   aff_t<fp_t> a;
   if (!jac_to_aff(a, soa_jac<fp_t>::ld(jac, ng, g))) { st[g] = ST_INF; return; }
-  if (!g1_in_subgroup(a)) { st[g] = ST_BAD; return; }
   soa_st_g1(out_aff, ng, g, a);
   st[g] = ST_OK;
 }
@@ -474,11 +492,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_sign(size_t n, con
                                                 uint8_t* __restrict__ out) {
   const size_t i = item_index<2>();
   if (i >= n) return;
-  uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
   aff_t<fp2p_t> c;
-  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   aff_t<fp2p_t> h;
   if (!jac_to_aff(h, g2_mul_cofactor(c))) {
     g2_compress(out + 96 * i, jac_infinity<fp2p_t>());
@@ -507,11 +524,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_out(size_t
   const size_t i = item_index<2>();
   if (i >= n) return;
   const int p = pr_odd() ? 1 : 0;
-  uint8_t scratch[BLS381_MSG_MAX + 9];
   uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
   aff_t<fp2p_t> c;
-  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, scratch);
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   aff_t<fp2p_t> h;
   if (!jac_to_aff(h, g2_mul_cofactor(c))) {
     g2_compress(comp + 96 * i, jac_infinity<fp2p_t>());
@@ -573,11 +589,10 @@ __global__ void __launch_bounds__(64, BLS_WAVES_PER_EU) k_hash_g2_pyecc(size_t n
   const size_t i = item_index<2>();
   if (i >= n) return;
   const int p = pr_odd() ? 1 : 0;
-  uint8_t sc[41];
-  uint8_t dom[8];
+    uint8_t dom[8];
   ld_bytes(dom, doms + 8 * i, 8);
   aff_t<fp2p_t> c;
-  hash_to_g2_candidate(c, msgs + 32 * i, 32, dom, sc);
+  hash_to_g2_candidate(c, msgs + 32 * i, 32, dom);
   const size_t ns = n * (size_t)H2_BITS;
   auto slot = [&](int b) { return i * (size_t)H2_BITS + b; };
   proj2<fp2p_t> cur;

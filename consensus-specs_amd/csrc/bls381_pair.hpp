@@ -274,13 +274,10 @@ __device__ inline void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
 // try-and-increment (bls_signature.md:74-86) before the cofactor: the even lane
 // hashes m || dom8 || 0x01 (x_re), the odd lane m || dom8 || 0x02 (x_im).
 __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* msg, uint32_t mlen,
-                                           const uint8_t dom8[8], uint8_t* scratch /* mlen + 9 */) {
+                                           const uint8_t dom8[8]) {
   const bool odd = pr_odd();
-  for (uint32_t i = 0; i < mlen; ++i) scratch[i] = msg[i];
-  for (int i = 0; i < 8; ++i) scratch[mlen + i] = dom8[i];
-  scratch[mlen + 8] = odd ? 2 : 1;
   uint32_t d[8];
-  sha256(d, scratch, mlen + 9);
+  sha256_msg_dom_tag(d, msg, mlen, dom8, odd ? 2 : 1);
   fp2p_t x;
   x.v = fp_to_mont(fp_plain_from_digest(d));
   const fp_t inc = fp_sel(odd, fp_zero(), FP_ONE_M);   // x += 1 (real part)

@@ -79,8 +79,16 @@ BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre&
 // final exponentiation removes.  Squarings of f are shared by all pairs.
 // One function per pair count; inside it the Fp12 squaring and line products
 // are inlined so f stays in registers for the whole loop.
+//
+// `degenerate` is set when some running point T_k reached infinity (Z = 0).
+// That happens only for a Q_k with no G2 component whose small order divides a
+// prefix of |x| (an order-13 point of E'(Fp2); DESIGN.md "Subgroup policy"):
+// T = -Q in an addition step gives Z = 0, and Z = 0 stays 0 through every later
+// step.  py_ecc's Miller loop then doubles the point at infinity, whose line
+// has a zero denominator, so its pairing value is 0 and the verdict False; the
+// kernels map the flag to that verdict.  Points of G2 never reach it.
 template <int N, class E>
-BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P) {
+BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bool& degenerate) {
   g2_proj<E> T[N];
   for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = e2_one<E>(); }
   fp12_g<E> f = fp12_one<E>();
@@ -101,13 +109,16 @@ BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P) {
       }
     }
   }
+  bool deg = false;
+  for (int k = 0; k < N; ++k) deg = deg | fp2_is_zero(T[k].z);   // no short circuit: pair-uniform DPP
+  degenerate = deg;
   return fp12_conj(f);
 }
 
 // runtime pair count (for verify_multiple chunks); pairs processed one at a time
 template <class E>
-BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P) {
-  return miller_loop_n<1>(&Q, &P);
+BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P, bool& degenerate) {
+  return miller_loop_n<1>(&Q, &P, degenerate);
 }
 
 // f^|x| in the cyclotomic subgroup by Granger-Scott squarings, then conjugate

@@ -10,6 +10,10 @@
 //   Fp 48 B;  Fp2 96 B = re || im;  Fp12 576 B = a0,a1,a2,b0,b1,b2 (each Fp2)
 //   G1 affine 96 B = x || y;  G2 affine 192 B = x || y (each Fp2)
 #include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
 
 #include "bls381_hash.hpp"
 #include "bls381_pairing.hpp"
@@ -122,10 +126,8 @@ int hc_g1_in_subgroup(const uint8_t* aff96) { return g1_in_subgroup(ldg1(aff96))
 int hc_g2_in_subgroup(const uint8_t* aff192) { return g2_in_subgroup(ldg2(aff192)); }
 
 int hc_hash_to_g2(const uint8_t* msg, uint32_t mlen, const uint8_t* dom8, uint8_t* aff192, uint8_t* comp96) {
-  uint8_t scratch[256 + 9];
-  if (mlen > 256) return -1;
   aff_t<fp2_t> c;
-  const int trials = hash_to_g2_candidate(c, msg, mlen, dom8, scratch);
+  const int trials = hash_to_g2_candidate(c, msg, mlen, dom8);
   aff_t<fp2_t> h;
   if (!jac_to_aff(h, g2_mul_cofactor(c))) return -2;
   st2(aff192, h.x); st2(aff192 + 96, h.y);
@@ -148,13 +150,111 @@ int hc_miller_loop(int n, const uint8_t* q192, const uint8_t* p96, uint8_t* o576
   if (n < 1 || n > 4) return -1;
   for (int k = 0; k < n; ++k) { Q[k] = ldg2(q192 + 192 * k); P[k] = g1_prepare(ldg1(p96 + 96 * k)); }
   fp12_t f;
+  bool degen = false;
   switch (n) {
-    case 1: f = miller_loop_n<1>(Q, P); break;
-    case 2: f = miller_loop_n<2>(Q, P); break;
-    case 3: f = miller_loop_n<3>(Q, P); break;
-    default: f = miller_loop_n<4>(Q, P); break;
+    case 1: f = miller_loop_n<1>(Q, P, degen); break;
+    case 2: f = miller_loop_n<2>(Q, P, degen); break;
+    case 3: f = miller_loop_n<3>(Q, P, degen); break;
+    default: f = miller_loop_n<4>(Q, P, degen); break;
   }
   st12(o576, f);
+  return degen ? 1 : 0;
+}
+
+// ---- whole-call semantics of the gfx950 pipelines, same headers, one thread
+// (bls381_capi.hip run_verify_batch / run_vm_batch): decode, the subgroup
+// policy (strict != 0: BLS381_POLICY_STRICT), py_ecc's infinity short circuit
+// (a pair with an infinite point is 1), a degenerate Miller loop -> False,
+// one final exponentiation.  Returns 1 / 0.
+static bool g1_in(const aff_t<fp_t>& a) { return g1_in_subgroup(a); }
+static bool g2_in(const aff_t<fp2_t>& a) { return g2_in_subgroup(a); }
+
+static int verify_pairs(int np, const aff_t<fp2_t>* Q, const aff_t<fp_t>* Pa) {
+  // pairs one Miller loop each (products of f), as k_miller_pairs_batch
+  fp12_t f = fp12_one<fp2_t>();
+  for (int k = 0; k < np; ++k) {
+    bool degen = false;
+    g1_line_pre P = g1_prepare(Pa[k]);
+    f = fp12_mul(f, miller_loop_n<1>(&Q[k], &P, degen));
+    if (degen) return 0;
+  }
+  return fp12_is_one(final_exp(f)) ? 1 : 0;
+}
+
+int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t mlen, const uint8_t* sig96, const uint8_t* dom8,
+              int strict) {
+  aff_t<fp_t> P;
+  aff_t<fp2_t> S;
+  const int sp = g1_decompress(P, pk48);
+  const int ss = g2_decompress(S, sig96);
+  if (sp == PT_BAD || ss == PT_BAD) return 0;
+  if (strict && ((sp == PT_OK && !g1_in(P)) || (ss == PT_OK && !g2_in(S)))) return 0;
+  aff_t<fp2_t> Q[2];
+  aff_t<fp_t> Pa[2];
+  int np = 0;
+  if (ss == PT_OK) {
+    Q[np] = S;
+    Pa[np].x = G1_GEN_X_M;
+    Pa[np].y = G1_GEN_NEGY_M;
+    ++np;
+  }
+  if (sp == PT_OK) {
+    aff_t<fp2_t> c;
+    hash_to_g2_candidate(c, msg, mlen, dom8);
+    if (jac_to_aff(Q[np], g2_mul_cofactor(c))) { Pa[np] = P; ++np; }
+  }
+  return verify_pairs(np, Q, Pa);
+}
+
+// n pubkeys / messages (mlen bytes each); pubkeys grouped by distinct message
+int hc_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, uint32_t mlen, const uint8_t* sig96,
+                       const uint8_t* dom8, int strict) {
+  std::map<std::string, jac_t<fp_t>> groups;
+  for (size_t i = 0; i < n; ++i) {
+    const std::string key((const char*)msgs + mlen * i, mlen);
+    auto it = groups.find(key);
+    if (it == groups.end()) it = groups.emplace(key, jac_infinity<fp_t>()).first;
+    aff_t<fp_t> a;
+    const int s = g1_decompress(a, pks + 48 * i);
+    if (s == PT_BAD || (s == PT_OK && strict && !g1_in(a))) return 0;
+    if (s == PT_OK) it->second = jac_add_aff(it->second, a);
+  }
+  aff_t<fp2_t> S;
+  const int ss = g2_decompress(S, sig96);
+  if (ss == PT_BAD || (ss == PT_OK && strict && !g2_in(S))) return 0;
+  std::vector<aff_t<fp2_t>> Q;
+  std::vector<aff_t<fp_t>> Pa;
+  for (auto& g : groups) {
+    aff_t<fp_t> a;
+    if (!jac_to_aff(a, g.second)) continue;
+    aff_t<fp2_t> c, h;
+    hash_to_g2_candidate(c, (const uint8_t*)g.first.data(), mlen, dom8);
+    if (!jac_to_aff(h, g2_mul_cofactor(c))) continue;
+    Q.push_back(h);
+    Pa.push_back(a);
+  }
+  if (ss == PT_OK) {
+    aff_t<fp_t> ng;
+    ng.x = G1_GEN_X_M;
+    ng.y = G1_GEN_NEGY_M;
+    Q.push_back(S);
+    Pa.push_back(ng);
+  }
+  return verify_pairs((int)Q.size(), Q.data(), Pa.data());
+}
+
+// n independent bls_verify calls (32-byte messages) on `threads` host threads:
+// the C++ CPU baseline line of bench.py (same arithmetic headers, g++ -O2)
+int hc_verify_batch_mt(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs, const uint8_t* dom8s,
+                       int strict, int threads, uint8_t* verdicts) {
+  if (threads < 1) threads = 1;
+  std::vector<std::thread> pool;
+  for (int t = 0; t < threads; ++t)
+    pool.emplace_back([=] {
+      for (size_t i = (size_t)t; i < n; i += (size_t)threads)
+        verdicts[i] = (uint8_t)hc_verify(pks + 48 * i, msgs32 + 32 * i, 32, sigs + 96 * i, dom8s + 8 * i, strict);
+    });
+  for (auto& th : pool) th.join();
   return 0;
 }
 
@@ -178,24 +278,24 @@ int hc_ssz_root(const uint8_t* item, const uint32_t* prog, uint32_t plen, uint8_
 
 #if defined(BLS_COUNT_OPS)
 // Per-stage Fp-multiplication counts of one bls_verify exactly as the gfx950
-// kernels of bls381_capi.hip stage it (decode_g1 + subgroup, decode_g2 +
-// subgroup, hash_to_g2, miller_loop_2, final_exp).  out[5] receives the counts.
+// kernels of bls381_capi.hip stage it (decode_g1 [+ subgroup check when strict],
+// decode_g2 [+ subgroup check], hash_to_g2, miller_loop_2, final_exp).  out[5]
+// receives the counts.
 int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint8_t* sig96, const uint8_t* dom8,
-                           uint64_t* out) {
+                           int strict, uint64_t* out) {
   aff_t<fp_t> P;
   aff_t<fp2_t> S, H;
   g_fp_mul_count = 0;
   int sp = g1_decompress(P, pk48);
-  if (sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
+  if (strict && sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
   out[0] = g_fp_mul_count;
   g_fp_mul_count = 0;
   int ss = g2_decompress(S, sig96);
-  if (ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
+  if (strict && ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
   out[1] = g_fp_mul_count;
   g_fp_mul_count = 0;
-  uint8_t scratch[41];
   aff_t<fp2_t> c;
-  hash_to_g2_candidate(c, msg32, 32, dom8, scratch);
+  hash_to_g2_candidate(c, msg32, 32, dom8);
   jac_to_aff(H, g2_mul_cofactor(c));
   out[2] = g_fp_mul_count;
   if (sp != PT_OK || ss != PT_OK) { out[3] = out[4] = 0; return -1; }
@@ -203,7 +303,8 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   aff_t<fp2_t> Q[2] = {S, H};
   aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
   g1_line_pre Pp[2] = {g1_prepare(ng), g1_prepare(P)};
-  const fp12_t f = miller_loop_n<2>(Q, Pp);
+  bool degen = false;
+  const fp12_t f = miller_loop_n<2>(Q, Pp, degen);
   out[3] = g_fp_mul_count;
   g_fp_mul_count = 0;
   const bool ok = fp12_is_one(final_exp(f));

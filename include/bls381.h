@@ -11,7 +11,7 @@
  *   - Plain pointers and sizes only; the caller owns every buffer.
  *   - Pubkeys are 48-byte compressed G1, signatures 96-byte compressed G2
  *     (specs/bls_signature.md:36-64).  Messages are `msg_len` bytes (the spec's
- *     message_hash is Bytes32; py_ecc hashes any length, so 0..MSG_MAX is accepted).
+ *     message_hash is Bytes32; py_ecc hashes any length, so 0..BLS381_MSG_MAX is accepted).
  *   - `dom8` is the 8-byte serialisation of the spec's uint64 `domain`
  *     (hash_to_G2, bls_signature.md:76-77).  The int -> bytes step is done by
  *     the caller so the byte order has one switch.
@@ -36,7 +36,18 @@ extern "C" {
 #define BLS381_EARG (-2)         /* bad argument (NULL, length) */
 #define BLS381_ENODEV (-3)       /* no HIP device / kernels not loadable */
 #define BLS381_EHIP (-4)         /* HIP runtime error */
-#define BLS381_MSG_MAX 256
+#define BLS381_MSG_MAX (1u << 20) /* message bytes per call (hash_to_G2 streams the message) */
+
+/* Subgroup policy of the verify paths (DESIGN.md "Subgroup policy").
+ *   PYECC (default): the checks py_ecc 1.7.0 makes, which the reference calls
+ *     (bls.py:24-31): decoding and the on-curve test only.  Torsion of order
+ *     prime to r in a pubkey leaves the verdict unchanged, and a signature with
+ *     no G2 component whose Miller loop degenerates gives False -- both as py_ecc.
+ *   STRICT: every pubkey and signature must also lie in G1 / G2, the spec's
+ *     "valid G1/G2 point" (specs/bls_signature.md:135-136,143-144).
+ * Aggregation never checks subgroups (py_ecc's aggregate_* do not). */
+#define BLS381_POLICY_PYECC 0
+#define BLS381_POLICY_STRICT 1
 
 /* ---- runtime ----------------------------------------------------------- */
 /* Number of visible HIP devices (0 if none). */
@@ -47,6 +58,11 @@ int bls381_init(int device);
 void bls381_shutdown(void);
 /* Last HIP error string of this thread (static storage). */
 const char* bls381_last_error(void);
+/* Process-wide subgroup policy (BLS381_POLICY_*), read when a call is queued.
+ * The Python shim sets it from bls.SUBGROUP_POLICY before each verify.
+ * Returns 0, or BLS381_EARG for an unknown policy.  Needs no device. */
+int bls381_set_subgroup_policy(int policy);
+int bls381_get_subgroup_policy(void);
 /* Kernel-time accounting (HIP events on the launch stream) for bench.py. */
 int bls381_profile_enable(int on);
 int bls381_profile_read(char* json_out, size_t cap);

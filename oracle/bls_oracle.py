@@ -681,6 +681,42 @@ def aggregate_pubkeys(pubkeys: Sequence[bytes]) -> bytes:
 
 
 # ---------------------------------------------------------------------------
+# Spec-strict subgroup policy -- NOT py_ecc's behaviour.  bls_signature.md:135-136
+# and :143-144 ask that each pubkey be "a valid G1 point" and the signature "a
+# valid G2 point"; py_ecc 1.7.0 checks only that they decode onto the curve.
+# These give the BLS381_POLICY_STRICT column of tests/golden/bls_torsion.json.
+# ---------------------------------------------------------------------------
+def in_G1(pt) -> bool:
+    return pt_is_inf(_FqOps, pt_multiply(_FqOps, pt, r))
+
+
+def in_G2(pt) -> bool:
+    return pt_is_inf(_Fq2Ops, pt_multiply(_Fq2Ops, pt, r))
+
+
+def verify_strict(message_hash: bytes, pubkey: bytes, signature: bytes, domain: int) -> bool:
+    try:
+        if not in_G1(pubkey_to_G1(pubkey)) or not in_G2(signature_to_G2(signature)):
+            return False
+    except (ValidationError, ValueError, AssertionError):
+        return False
+    return verify(message_hash, pubkey, signature, domain)
+
+
+def verify_multiple_strict(pubkeys: Sequence[bytes], message_hashes: Sequence[bytes],
+                           signature: bytes, domain: int) -> bool:
+    if len(pubkeys) != len(message_hashes):
+        raise ValidationError(
+            "len(pubkeys) (%s) should be equal to len(message_hashes) (%s)" % (len(pubkeys), len(message_hashes)))
+    try:
+        if not all(in_G1(pubkey_to_G1(p)) for p in pubkeys) or not in_G2(signature_to_G2(signature)):
+            return False
+    except (ValidationError, ValueError, AssertionError):
+        return False
+    return verify_multiple(pubkeys, message_hashes, signature, domain)
+
+
+# ---------------------------------------------------------------------------
 # Helpers used by fixture generation and tests
 # ---------------------------------------------------------------------------
 def g2_projective_to_hex(pt) -> List[List[str]]:

@@ -31,3 +31,12 @@ def native():
     from bls381_amd import _native
     _native.init(0)
     return _native
+
+
+@pytest.fixture(scope="session")
+def torsion():
+    """tests/golden/bls_torsion.json (make_torsion_vectors.py): points outside G1/G2,
+    with py_ecc and spec-strict verdict columns."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "bls_torsion.json")) as f:
+        return json.load(f)

@@ -551,3 +551,85 @@ def test_verify_deposits_pipeline(native):
         assert O.verify(S.signing_root(S.DepositData, {"pubkey": v[:48], "withdrawal_credentials": v[48:80],
                                                        "amount": int.from_bytes(v[80:88], "little"),
                                                        "signature": v[88:]}), v[:48], v[88:], dom) == want[k]
+
+
+# ------------------------------- subgroup policy on torsion points
+def _vm_args(c):
+    return ([bytes.fromhex(p) for p in c["pubkeys"]], [bytes.fromhex(m) for m in c["messages"]],
+            bytes.fromhex(c["signature"]), int(c["domain"]))
+
+
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_torsion_verdicts_both_policies(native, torsion, policy):
+    """Points with small-order components: py_ecc's verdicts under SUBGROUP_POLICY="pyecc"
+    (incl. the degenerate Miller loop of an order-13 signature), the spec-strict ones under
+    "strict" -- through the shim, the verify batch, the verify_multiple batch and the
+    sharded partial products."""
+    from bls381_amd import bls
+    col = "expected_" + policy
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = policy
+    try:
+        vs = torsion["verify"]
+        for c in vs:
+            got = bls.bls_verify(bytes.fromhex(c["pubkey"]), bytes.fromhex(c["message"]),
+                                 bytes.fromhex(c["signature"]), int(c["domain"]))
+            assert got == c[col], (c["kind"], policy)
+        native.set_subgroup_policy(policy)
+        v = native.verify_batch(b"".join(bytes.fromhex(c["pubkey"]) for c in vs),
+                                b"".join(bytes.fromhex(c["message"]) for c in vs),
+                                b"".join(bytes.fromhex(c["signature"]) for c in vs),
+                                b"".join(int(c["domain"]).to_bytes(8, "big") for c in vs))
+        assert list(v) == [c[col] for c in vs]
+        vms = torsion["verify_multiple"]
+        for c in vms:
+            assert bls.bls_verify_multiple(*_vm_args(c)) == c[col], (c["kind"], policy)
+        native.set_subgroup_policy(policy)
+        off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+        for c in vms:
+            p, m, s, d = _vm_args(c)
+            pks += b"".join(p); msgs += b"".join(m); sigs += s; doms += d.to_bytes(8, "big")
+            off.append(off[-1] + len(p))
+        assert list(native.verify_multiple_batch(off, pks, msgs, 32, sigs, doms)) == [c[col] for c in vms]
+        for c in vms:                                  # two-shard partial products
+            p, m, s, d = _vm_args(c)
+            d8 = d.to_bytes(8, "big")
+            rc0, a = native.miller_partial(b"".join(p[:1]), b"".join(m[:1]), 32, s, True, d8)
+            rc1, b = native.miller_partial(b"".join(p[1:]), b"".join(m[1:]), 32, s, False, d8)
+            got = (rc0 == 0 and rc1 == 0) and native.final_verify(a + b)
+            if len(set(m)) == len(m):                  # shards split whole message groups only
+                assert got == c[col], (c["kind"], policy)
+    finally:
+        bls.SUBGROUP_POLICY = old
+        native.set_subgroup_policy(old)
+
+
+def test_torsion_aggregates(native, torsion):
+    """Aggregation never checks subgroups: sums with torsion components are py_ecc's bytes."""
+    from bls381_amd import bls
+    for c in torsion["aggregate_pubkeys"]:
+        assert bls.bls_aggregate_pubkeys([bytes.fromhex(p) for p in c["input"]]).hex() == c["output"], c["kind"]
+    for c in torsion["aggregate_sigs"]:
+        assert bls.bls_aggregate_signatures([bytes.fromhex(s) for s in c["input"]]).hex() == c["output"], c["kind"]
+
+
+def test_long_and_mixed_length_messages(native):
+    """py_ecc hashes messages of any length: > 256 bytes (streamed SHA-256, multi-block), and
+    a verify_multiple mixing lengths (per-length partial products, one final exponentiation)."""
+    from bls381_amd import bls
+    sk = 4242
+    for n in (257, 1000, 4096):
+        msg = bytes((7 * i) & 0xFF for i in range(n))
+        sig = bls.bls_sign(msg, sk, 11)
+        assert sig == O.sign(msg, sk, 11)
+        assert bls.bls_verify(bls.privtopub(sk), msg, sig, 11) is True
+        assert bls.bls_verify(bls.privtopub(sk), msg[:-1], sig, 11) is False
+    sks = [5, 6, 7, 8]
+    msgs = [b"\x01" * 32, b"\x02" * 300, b"", b"\x01" * 32]
+    pks = [bls.privtopub(k) for k in sks]
+    sig = bls.bls_aggregate_signatures([bls.bls_sign(m, k, 2) for m, k in zip(msgs, sks)])
+    assert O.verify_multiple(pks, msgs, sig, 2) is True
+    assert bls.bls_verify_multiple(pks, msgs, sig, 2) is True
+    assert bls.bls_verify_multiple(pks[::-1], msgs, sig, 2) is False
+    with pytest.raises(ValueError):
+        bls.bls_verify(pks[0], bytes((1 << 20) + 1), sig, 2)

@@ -73,6 +73,12 @@ def model_batch(call_off, pks, msgs, mlen, sigs, dom8s):
     return out
 
 
+def model_mixed(pks, msgs, sig, dom8):
+    """CPU stand-in for one mixed-length call (bls.verify_multiple_bytes)."""
+    import bls_oracle as O
+    return O.verify_multiple(pks, msgs, sig, int.from_bytes(dom8, "big"))
+
+
 def _oracle_agg(pks):
     import bls_oracle as O
     return O.aggregate_pubkeys([pks[48 * i:48 * i + 48] for i in range(len(pks) // 48)])
@@ -94,7 +100,8 @@ def _worker(rank, world, port, case, q, kind="vm"):
         except ValueError:
             v = "ValueError"
     else:
-        v = sharding.sharded_verify_multiple_batch(case, rank=rank, world=world, batch_fn=model_batch)
+        v = sharding.sharded_verify_multiple_batch(case, rank=rank, world=world, batch_fn=model_batch,
+                                                   mixed_fn=model_mixed)
     q.put((rank, v))
     dist.barrier()
     dist.destroy_process_group()
@@ -145,6 +152,18 @@ def test_sharded_verify_multiple_gloo_world2(case):
     assert res == {0: False, 1: False}
 
 
+def test_sharded_verify_multiple_mixed_lengths_gloo_world2():
+    """Messages of several lengths in one call: one partial per length per rank, one FE."""
+    import bls_oracle as O
+    sks = [11, 22, 33, 44, 55]
+    msgs = [b"\x01" * 32, b"\x02" * 20, b"\x01" * 32, b"\x03" * 40, b""]
+    pks = [O.privtopub(k) for k in sks]
+    sig = O.aggregate_signatures([O.sign(m, k, 5) for m, k in zip(msgs, sks)])
+    assert O.verify_multiple(pks, msgs, sig, 5) is True
+    assert _run((pks, msgs, sig, 5)) == {0: True, 1: True}
+    assert _run((pks, msgs[:4] + [b"x"], sig, 5)) == {0: False, 1: False}
+
+
 def test_shard_range_covers_everything():
     from bls381_amd.sharding import shard_range
     for n in (0, 1, 5, 8, 1 << 20):
@@ -181,7 +200,9 @@ def test_sharded_verify_multiple_batch_gloo_world2(case):
         (pks[:1], msgs[:1], O.sign(msgs[0], 11, 5), 6),        # wrong domain
         ([], [], O.sign(msgs[0], 11, 5), 7),                    # empty call, non-infinite signature
         (pks[:1], [b"\x01" * 31], O.sign(msgs[0], 11, 5), 5),  # other message length
+        (pks[:2], [msgs[0], b"\x07" * 7],                      # mixed lengths in one call
+         O.aggregate_signatures([O.sign(msgs[0], 11, 5), O.sign(b"\x07" * 7, 22, 5)]), 5),
     ]
-    want = [True, True, False, False, False]
+    want = [True, True, False, False, False, True]
     res = _run(calls, kind="batch")
     assert res == {0: want, 1: want}

@@ -1,0 +1,140 @@
+"""Subgroup policy on the CPU: torsion fixtures vs the oracle, and the whole-call
+semantics of the device headers (host g++ build) under both policies.
+
+py_ecc 1.7.0 (reference path: eth2spec/utils/bls.py:24-31) never checks that a
+point lies in G1 / G2; the spec asks for valid group points
+(specs/bls_signature.md:135-136,143-144).  tests/golden/bls_torsion.json holds
+both verdict columns; the engine's BLS381_POLICY_PYECC must give the first and
+BLS381_POLICY_STRICT the second.  The GPU side of the same check is
+tests/test_gpu_parity.py::test_torsion_*.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+
+import bls_oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    import build_native
+    return ctypes.CDLL(os.environ.get("BLS381_HOSTCHECK_LIB") or build_native.build_hostcheck())
+
+
+def _h(s):
+    return bytes.fromhex(s)
+
+
+def test_torsion_fixtures_match_oracle(torsion):
+    """Recompute a spread of the committed verdicts (one in three verify cases, every
+    verify_multiple case) and every aggregate with the oracle."""
+    for c in torsion["verify"][::3]:
+        a = (_h(c["message"]), _h(c["pubkey"]), _h(c["signature"]), int(c["domain"]))
+        assert O.verify(*a) == c["expected_pyecc"], c["kind"]
+        assert O.verify_strict(*a) == c["expected_strict"], c["kind"]
+    for c in torsion["verify_multiple"]:
+        a = ([_h(p) for p in c["pubkeys"]], [_h(m) for m in c["messages"]], _h(c["signature"]), int(c["domain"]))
+        assert O.verify_multiple(*a) == c["expected_pyecc"], c["kind"]
+        assert O.verify_multiple_strict(*a) == c["expected_strict"], c["kind"]
+    for c in torsion["aggregate_pubkeys"]:
+        assert O.aggregate_pubkeys([_h(p) for p in c["input"]]).hex() == c["output"], c["kind"]
+    for c in torsion["aggregate_sigs"]:
+        assert O.aggregate_signatures([_h(s) for s in c["input"]]).hex() == c["output"], c["kind"]
+
+
+def test_torsion_fixtures_cover_both_divergences(torsion):
+    """The file pins each way the policies differ: True under py_ecc and False under
+    strict (G1 torsion), and the degenerate Miller loop of an order-13 signature."""
+    kinds = {c["kind"]: c for c in torsion["verify"]}
+    assert kinds["pk_order3_sig_inf"]["expected_pyecc"] and not kinds["pk_order3_sig_inf"]["expected_strict"]
+    assert kinds["pk_G_plus_T3"]["expected_pyecc"] and not kinds["pk_G_plus_T3"]["expected_strict"]
+    assert not kinds["sig_T13_pk_inf"]["expected_pyecc"]
+    vm = {c["kind"]: c for c in torsion["verify_multiple"]}
+    assert vm["group_torsion_cancels"]["expected_pyecc"] and not vm["group_torsion_cancels"]["expected_strict"]
+
+
+def _host_verify(L, c, strict):
+    m = _h(c["message"])
+    return L.hc_verify(_h(c["pubkey"]), m, len(m), _h(c["signature"]), int(c["domain"]).to_bytes(8, "big"), strict)
+
+
+def _host_verify_multiple(L, c, strict):
+    pks = b"".join(_h(p) for p in c["pubkeys"])
+    msgs = b"".join(_h(m) for m in c["messages"])
+    return L.hc_verify_multiple(len(c["pubkeys"]), pks or None, msgs or None, 32, _h(c["signature"]),
+                                int(c["domain"]).to_bytes(8, "big"), strict)
+
+
+@pytest.mark.parametrize("strict", [0, 1])
+def test_host_pipeline_torsion_verdicts(L, torsion, strict):
+    """The device headers' pipeline semantics (policy, degenerate loop -> False) on the host."""
+    col = "expected_strict" if strict else "expected_pyecc"
+    for c in torsion["verify"]:
+        assert _host_verify(L, c, strict) == int(c[col]), (c["kind"], strict)
+    for c in torsion["verify_multiple"]:
+        assert _host_verify_multiple(L, c, strict) == int(c[col]), (c["kind"], strict)
+
+
+@pytest.mark.parametrize("strict", [0, 1])
+def test_host_pipeline_golden_verdicts(L, golden, strict):
+    """The ordinary golden batches have the same verdicts under either policy."""
+    _, gb = golden
+    for c in gb["verify"]:
+        assert _host_verify(L, c, strict) == int(c["expected"]), c["kind"]
+    for c in gb["verify_multiple"]:
+        if len(c["pubkeys"]) != len(c["messages"]):
+            continue
+        assert _host_verify_multiple(L, c, strict) == int(c["expected"]), c["kind"]
+
+
+_ASAN_RUNNER = r"""
+import ctypes, json, sys
+L = ctypes.CDLL(sys.argv[1])
+with open(sys.argv[2]) as f: gb = json.load(f)
+with open(sys.argv[3]) as f: tor = json.load(f)
+h = bytes.fromhex
+bad = 0
+for src, col in ((gb, "expected"), (tor, "expected_pyecc")):
+    for c in src["verify"]:
+        m = h(c["message"])
+        v = L.hc_verify(h(c["pubkey"]), m, len(m), h(c["signature"]), int(c["domain"]).to_bytes(8, "big"), 0)
+        bad += v != int(c[col])
+    for c in src["verify_multiple"]:
+        if len(c["pubkeys"]) != len(c["messages"]):
+            continue
+        pks = b"".join(h(p) for p in c["pubkeys"]) or None
+        ms = b"".join(h(x) for x in c["messages"]) or None
+        v = L.hc_verify_multiple(len(c["pubkeys"]), pks, ms, 32, h(c["signature"]),
+                                 int(c["domain"]).to_bytes(8, "big"), 0)
+        bad += v != int(c[col])
+print("mismatches", bad)
+sys.exit(1 if bad else 0)
+"""
+
+
+def test_sanitized_host_build_over_golden_batches(tmp_path):
+    """ASan + UBSan build of the device headers (host) over every golden and torsion
+    verify / verify_multiple case: no sanitizer report, same verdicts."""
+    import build_native
+    lib = build_native.build_hostcheck(sanitize=True)
+    asan = subprocess.run(["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()
+    ubsan = subprocess.run(["gcc", "-print-file-name=libubsan.so"], capture_output=True, text=True).stdout.strip()
+    if not os.path.isabs(asan) or not os.path.exists(asan):
+        pytest.skip("libasan runtime not found")
+    runner = tmp_path / "run.py"
+    runner.write_text(_ASAN_RUNNER)
+    env = dict(os.environ, LD_PRELOAD=" ".join(p for p in (asan, ubsan) if os.path.isabs(p)),
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    g = os.path.join(ROOT, "tests", "golden")
+    res = subprocess.run([sys.executable, str(runner), lib, os.path.join(g, "bls_golden_batches.json"),
+                          os.path.join(g, "bls_torsion.json")], env=env, capture_output=True, text=True,
+                         timeout=600)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    assert "ERROR: AddressSanitizer" not in res.stderr and "runtime error" not in res.stderr, res.stderr[-4000:]
+    assert "mismatches 0" in res.stdout
