@@ -213,6 +213,11 @@ VerifyWs carve_verify(void* ws, size_t n) {
 
 // 1: decode_g2 runs on the side stream after decode_g1 (r01k: 1.59-1.61 M ->
 // 1.62 M verifications/s on one box); 0: on the main stream before hash_to_g2
+// 1: the bls_verify Miller loop runs on lane quads (k_miller_verify_q), 0: lane pairs
+#ifndef BLS_ML_QUAD
+#define BLS_ML_QUAD 0
+#endif
+
 #ifndef BLS_DECODE_G2_SIDE
 #define BLS_DECODE_G2_SIDE 1
 #endif
@@ -239,8 +244,14 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
 #endif
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+#if BLS_ML_QUAD
+  LAUNCH("miller_loop_2", s, dim3(grid_for(4 * n)), b, k_miller_verify_q, n, (const uint32_t*)w.sig_aff,
+         (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f,
+         w.f_st);
+#else
   LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
          (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
+#endif
   LAUNCH("final_exp", s, g2, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
   return 0;
 }

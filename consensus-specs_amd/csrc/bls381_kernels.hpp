@@ -8,6 +8,7 @@
 //                    base[(c*14 + k) * 2n + 2i + p]   (lane index 2i + p)
 #pragma once
 #include "bls381_pair.hpp"
+#include "bls381_quad.hpp"
 #include "bls381_ssz.hpp"
 
 namespace bls381 {
@@ -192,6 +193,52 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(s
   else f = fp12_one<fp2p_t>();
   soa_st12(f_out, n, i, f);
   // a degenerate loop is py_ecc's zero pairing value: verdict False
+  if (lead) st_out[i] = degen ? ST_BAD : ST_OK;
+}
+
+// The same verify on a lane quad (bls381_quad.hpp): the lo half runs the pair
+// (sig, -g1), the hi half (H(m), pk), side by side; a single finite pair runs on
+// lo with the hi half idle.  f is stored in the layout of k_miller_verify (each
+// half writes its three Fp2 components), so the final exponentiation is shared.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_q(size_t n, const uint32_t* __restrict__ sig_aff,
+                                                           const uint8_t* __restrict__ sig_st,
+                                                           const uint32_t* __restrict__ pk_aff,
+                                                           const uint8_t* __restrict__ pk_st,
+                                                           const uint32_t* __restrict__ h_aff,
+                                                           uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t i = item_index<4>();
+  if (i >= n) return;
+  const bool hi = qd_hi();
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const size_t lp = 2 * i + (pr_odd() ? 1 : 0);   // this lane's coefficient slot of item i
+  const uint8_t ss = sig_st[i], ps = pk_st[i];
+  if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
+  const bool sig_ok = ss == ST_OK, pk_ok = ps == ST_OK;
+  fq12_t f;
+  bool degen = false;
+  if (sig_ok || pk_ok) {
+    // lo: the signature pair if finite, else the pubkey pair; hi: the pubkey pair when both are
+    // finite, else an idle copy of lo's pair (valid operands, its lines masked to 1)
+    const bool active = hi ? (sig_ok && pk_ok) : true;
+    const bool use_pk = (hi && active) || !sig_ok;
+    aff_t<fp2p_t> Q;
+    aff_t<fp_t> P;
+    const uint32_t* qsrc = use_pk ? h_aff : sig_aff;
+    Q.x = pr_make(soa_ld(qsrc, 2 * n, lp, 0));
+    Q.y = pr_make(soa_ld(qsrc, 2 * n, lp, 1));
+    if (use_pk) {
+      P = soa_ld_g1(pk_aff, n, i);
+    } else {
+      P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M;
+    }
+    f = miller_loop_quad(Q, g1_prepare(P), active, degen);
+  } else {
+    f = fq12_one();
+  }
+  const int c0 = hi ? 3 : 0;
+  soa_st(f_out, 2 * n, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * n, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * n, lp, c0 + 2, f.h.c2.v);
   if (lead) st_out[i] = degen ? ST_BAD : ST_OK;
 }
 

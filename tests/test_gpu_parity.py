@@ -633,3 +633,74 @@ def test_long_and_mixed_length_messages(native):
     assert bls.bls_verify_multiple(pks[::-1], msgs, sig, 2) is False
     with pytest.raises(ValueError):
         bls.bls_verify(pks[0], bytes((1 << 20) + 1), sig, 2)
+
+
+# ---------------------------------------------- C4 / C5 at full size
+def test_c4_aggregate_2p20_keys_eight_shards(native):
+    """C4: 2^20 pubkeys aggregated as 8 shards (sharding.shard_range, one per GPU of a node),
+    each a device partial, the partials summed: equals [sum k]G in closed form (the keys are
+    [(i mod 64) + 1]G), and equals the unsharded aggregation."""
+    from bls381_amd.sharding import shard_range
+    n, world = 1 << 20, 8
+    base = native.privtopub_batch(b"".join(k.to_bytes(32, "big") for k in range(1, 65)))
+    keys = np.frombuffer(base, dtype=np.uint8).reshape(64, 48)[np.arange(n) % 64].tobytes()
+    parts = []
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        parts.append(native.aggregate_pubkeys(keys[48 * lo:48 * hi]))
+    total = native.aggregate_pubkeys(b"".join(parts))
+    want = sum((i % 64) + 1 for i in range(n)) % O.r
+    assert total == O.privtopub(want)
+    assert native.aggregate_pubkeys(keys) == total
+
+
+def test_c4_verify_multiple_batch_eight_shards(native, golden):
+    """C4 second half: independent verify_multiple calls split into 8 contiguous call ranges
+    (sharding.shard_range); the per-shard batch verdicts, concatenated, equal the oracle's."""
+    from bls381_amd.sharding import shard_range
+    _, gb = golden
+    cases = [c for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])] * 9
+    world = 8
+    got = []
+    for r in range(world):
+        lo, hi = shard_range(len(cases), r, world)
+        off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+        for c in cases[lo:hi]:
+            pks += b"".join(bytes.fromhex(p) for p in c["pubkeys"])
+            msgs += b"".join(bytes.fromhex(m) for m in c["messages"])
+            sigs += bytes.fromhex(c["signature"])
+            doms += int(c["domain"]).to_bytes(8, "big")
+            off.append(off[-1] + len(c["pubkeys"]))
+        got.extend(native.verify_multiple_batch(off, pks, msgs, 32, sigs, doms))
+    assert got == [c["expected"] for c in cases]
+
+
+def test_c5_verify_multiple_4096_messages(native):
+    """C5 at L = 4096: signatures from the engine spot-checked against the oracle, the
+    aggregate signature over all 4096 (message, key) pairs verifies, a swapped key, a changed
+    message or domain does not; the two-shard partial products agree."""
+    from bls381_amd import bls
+    rng = random.Random(0xB15_C5)
+    L = 4096
+    sks = [rng.randrange(1, O.r) for _ in range(L)]
+    msgs = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(L)]
+    skb = b"".join(k.to_bytes(32, "big") for k in sks)
+    pks = native.privtopub_batch(skb)
+    sigs = native.sign_batch(b"".join(msgs), skb, (1).to_bytes(8, "big") * L)
+    for j in (0, 1777, L - 1):
+        assert sigs[96 * j:96 * j + 96] == O.sign(msgs[j], sks[j], 1)
+        assert pks[48 * j:48 * j + 48] == O.privtopub(sks[j])
+    sig = native.aggregate_signatures(sigs)
+    pk_list = [pks[48 * j:48 * j + 48] for j in range(L)]
+    assert bls.bls_verify_multiple(pk_list, msgs, sig, 1) is True
+    assert bls.bls_verify_multiple(pk_list, msgs, sig, 2) is False
+    swapped = pk_list[:]
+    swapped[5], swapped[6] = swapped[6], swapped[5]
+    assert bls.bls_verify_multiple(swapped, msgs, sig, 1) is False
+    changed = msgs[:]
+    changed[4000] = bytes([changed[4000][0] ^ 1]) + changed[4000][1:]
+    assert bls.bls_verify_multiple(pk_list, changed, sig, 1) is False
+    d8 = (1).to_bytes(8, "big")
+    rc0, a = native.miller_partial(pks[:48 * 2048], b"".join(msgs[:2048]), 32, sig, True, d8)
+    rc1, b = native.miller_partial(pks[48 * 2048:], b"".join(msgs[2048:]), 32, sig, False, d8)
+    assert rc0 == 0 and rc1 == 0 and native.final_verify(a + b) is True
