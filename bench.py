@@ -57,11 +57,14 @@ def parse():
     ap.add_argument("--committee-size", type=int, default=128)
     ap.add_argument("--cpu-sample", type=int, default=256)
     ap.add_argument("--cpu-procs", type=int, default=16)
+    ap.add_argument("--cpp-sample", type=int, default=2048, help="items for the C++ host-build CPU line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4/C5 lines")
     ap.add_argument("--c4-keys", type=int, default=1 << 17, help="pubkeys per GPU in the C4 aggregation")
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
+    ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
+                    help="subgroup policy of the headline line (bls.SUBGROUP_POLICY)")
     return ap.parse_args()
 
 
@@ -164,6 +167,19 @@ def cpu_baseline(pks, msgs, sigs, sample, procs):
     return sample / dt, res, dt
 
 
+def cpu_baseline_cpp(pks, msgs, sigs, doms, sample, threads):
+    """The g++ build of the engine's own arithmetic headers (host_check.cpp hc_verify: same
+    decode / hash_to_G2 / Miller loop / final exponentiation code as the kernels, scalar
+    x86-64) on `threads` host threads, bounded sample: the stronger CPU line."""
+    import build_native
+    L = ctypes.CDLL(build_native.build_hostcheck())
+    out = (ctypes.c_uint8 * sample)()
+    t0 = time.perf_counter()
+    L.hc_verify_batch_mt(ctypes.c_size_t(sample), pks, msgs, sigs, doms, 0, threads, out)
+    dt = time.perf_counter() - t0
+    return sample / dt, [bool(v) for v in out], dt
+
+
 R_ORDER = 0x73eda753299d7d483339d80809a1d80553bda402fffe5bfeffffffff00000001
 INF_G1 = bytes([0xC0]) + bytes(47)
 
@@ -202,17 +218,25 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
     msgs = b"".join(bytes(m0[32 * c:32 * c + 32]) + m1[32 * c:32 * c + 32] for c in range(nc))
     call_off = np.arange(0, 2 * nc + 1, 2, dtype=np.uint32)
     doms = (2).to_bytes(8, "big") * nc
+    d_sigs, d_doms = t_u8(sigs), t_u8(doms)
+    d_ver = torch.zeros(nc, dtype=torch.uint8, device=dev)
+    vws = torch.empty(L.bls381_verify_multiple_batch_workspace_size(nc, 2 * nc, 32), dtype=torch.uint8, device=dev)
 
     def step():
+        # aggregates stay in HBM: bls_aggregate_pubkeys -> bls_verify_multiple on device buffers, one stream
         native.check(L.bls381_aggregate_pubkeys_batch_device(
             2 * nc, offsets.ctypes.data_as(ctypes.c_void_p), nc * cs, d_cpks.data_ptr(), d_out.data_ptr(),
             d_st.data_ptr(), aws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
-        aggs = d_out.cpu().numpy().tobytes()          # synchronises the aggregation
-        return native.verify_multiple_batch(call_off, aggs, msgs, 32, sigs, doms)
+        native.check(L.bls381_verify_multiple_batch_device(
+            nc, call_off.ctypes.data_as(ctypes.c_void_p), msgs, 32, d_out.data_ptr(), d_sigs.data_ptr(),
+            d_doms.data_ptr(), d_ver.data_ptr(), vws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
 
-    got = step()
-    assert np.array_equal(got, expected), "C3 verdict mismatch"
+    step()
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ver.cpu().numpy().astype(bool), expected), "C3 verdict mismatch"
     assert int(d_st.abs().sum().item()) == 0
+    host = native.verify_multiple_batch(call_off, d_out.cpu().numpy().tobytes(), msgs, 32, sigs, doms)
+    assert np.array_equal(host, expected), "C3 host-path verdict mismatch"
     steps = max(args.steps, 3)
     if world > 1:
         dist.barrier()
@@ -223,7 +247,8 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
     torch.cuda.synchronize()
     t = _max_time(time.perf_counter() - t0, world, dist, dev)
     return {"workload": "C3: %d committees x %d per GPU: 2 x bls_aggregate_pubkeys + bls_verify_multiple([agg, inf], "
-                        "[m0, m1], sig, 2) each, 1/16 wrong message; verify_multiple batch on host buffers" % (nc, cs),
+                        "[m0, m1], sig, 2) each, 1/16 wrong message; device-resident (aggregates never leave HBM)"
+                        % (nc, cs),
             "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world}
 
 
@@ -473,6 +498,7 @@ def main():
     from bls381_amd import _native as native
     native.init(local_rank)
     L = native.lib()
+    native.set_subgroup_policy(args.policy)
 
     # ---------------- workload, device-resident
     n = args.n
@@ -515,6 +541,25 @@ def main():
         elapsed = float(t.item())
     total_items = n * args.steps * world
     value = total_items / elapsed
+
+    # the same batch under the other subgroup policy (same verdicts: no torsion points in it)
+    other = None
+    if not args.no_secondary:
+        pol = "strict" if args.policy == "pyecc" else "pyecc"
+        native.set_subgroup_policy(pol)
+        step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ot = _max_time(time.perf_counter() - t0, world, dist, dev)
+        assert np.array_equal(d_ver.cpu().numpy().astype(bool), expected), "verdict mismatch under " + pol
+        other = {"subgroup_policy": pol, "verifications_per_s": n * args.steps * world / ot,
+                 "ms_per_step": 1e3 * ot / args.steps}
+        native.set_subgroup_policy(args.policy)
 
     # ---------------- committee aggregation (C3 shape), device-resident
     agg = None
@@ -571,7 +616,7 @@ def main():
         return
 
     # ---------------- roofline of the dominant kernel (live HIP-event times)
-    counts = count_fp_muls(pks, msgs, sigs, doms)
+    counts = count_fp_muls(pks, msgs, sigs, doms, strict=int(args.policy == "strict"))
     kern_ms = {k: v["total_ms"] / v["count"] for k, v in prof.items()}
     dom_k = max(kern_ms, key=kern_ms.get)
     peak, peak_src = load_valu_peak()
@@ -600,6 +645,16 @@ def main():
                          "algorithm restatement: Fq12-coordinate Miller loop, naive final exponentiation), "
                          "multiprocessing.Pool(%d), %.1f s wall" % (args.cpu_sample, args.cpu_procs, dt)}
 
+    cpu_cpp = None
+    if world == 1 and not args.no_cpu_baseline:
+        k = min(args.cpp_sample, n)
+        rate, res, dt = cpu_baseline_cpp(pks[:48 * k], msgs[:32 * k], sigs[:96 * k], doms[:8 * k], k, args.cpu_procs)
+        assert res == list(expected[:k]), "C++ host build disagrees with GPU verdicts"
+        cpu_cpp = {"value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
+                   "sample": "first %d items of the same C2 batch, C++ host build of the engine's arithmetic headers "
+                             "(g++ -O2, host_check.cpp hc_verify_batch_mt), %d std::threads, %.1f s wall"
+                             % (k, args.cpu_procs, dt)}
+
     line = {
         "metric": "BLS sig verifications/sec (whole node)",
         "value": round(value, 2),
@@ -614,9 +669,12 @@ def main():
         "dtype": "u32 (381-bit Montgomery, 14x28-bit limbs in u32 words)",
         "data": "synthetic (random keys/messages, signatures made on device)",
         "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
-                   "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world},
+                   "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world,
+                   "subgroup_policy": args.policy},
+        "other_policy": other,
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "cpu_baseline_cpp": cpu_cpp,
         "aggregation": agg,
     }
     line.update(sec)

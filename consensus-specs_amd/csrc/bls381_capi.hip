@@ -213,9 +213,11 @@ VerifyWs carve_verify(void* ws, size_t n) {
 
 // 1: decode_g2 runs on the side stream after decode_g1 (r01k: 1.59-1.61 M ->
 // 1.62 M verifications/s on one box); 0: on the main stream before hash_to_g2
-// 1: the bls_verify Miller loop runs on lane quads (k_miller_verify_q), 0: lane pairs
-#ifndef BLS_ML_QUAD
-#define BLS_ML_QUAD 0
+// bls_verify batches of at most this many items run their Miller loops on lane quads
+// (k_miller_verify_q: 4n lanes <= one wave per SIMD of the 1024), larger ones on lane
+// pairs (k_miller_verify: 13% less work per item, measured at 2^16 items)
+#ifndef BLS_ML_QUAD_MAX_N
+#define BLS_ML_QUAD_MAX_N 16384
 #endif
 
 #ifndef BLS_DECODE_G2_SIDE
@@ -244,14 +246,16 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
 #endif
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
-#if BLS_ML_QUAD
-  LAUNCH("miller_loop_2", s, dim3(grid_for(4 * n)), b, k_miller_verify_q, n, (const uint32_t*)w.sig_aff,
-         (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f,
-         w.f_st);
-#else
-  LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
-         (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
-#endif
+  if (n <= BLS_ML_QUAD_MAX_N) {
+    // latency path: one item per lane quad, its two pairs side by side (half the per-item latency,
+    // ~13% more work per item -- the better trade while the batch leaves SIMDs idle)
+    LAUNCH("miller_loop_2q", s, dim3(grid_for(4 * n)), b, k_miller_verify_q, n, (const uint32_t*)w.sig_aff,
+           (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+           w.f, w.f_st);
+  } else {
+    LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
+           (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
+  }
   LAUNCH("final_exp", s, g2, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
   return 0;
 }
@@ -349,17 +353,25 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
 // Host plan for a batch of bls_verify_multiple calls.  Within each call the
 // pubkeys are grouped by distinct message (first-appearance order), as py_ecc's
 // verify_multiple does; every group becomes one pair
-// (hash_to_G2(m), sum of its pubkeys), and each call adds (sig, -g1).
+// (hash_to_G2(m), sum of its pubkeys) and each call adds (sig, -g1).  When the
+// key bytes are on the host, a group whose keys are all the canonical infinity
+// encoding and an infinite signature are dropped (py_ecc's pairing with an
+// infinite point is 1).  A call's pairs run two at a time on lane quads
+// (k_miller_quads: one pair per half, shared squarings); a call with several
+// quads multiplies them in segmented product passes; one final exponentiation
+// per call.
+constexpr int32_t PAIR_NONE = INT32_MIN;
+
 struct VmPlan {
-  size_t n_calls = 0, G = 0, npairs = 0;
-  std::vector<uint8_t> pks_perm;        // pubkeys reordered by group
-  std::vector<uint32_t> group_off;      // G + 1 offsets into pks_perm (in keys)
+  size_t n_calls = 0, n_keys = 0, G = 0, nquads = 0;
+  std::vector<uint32_t> key_idx;        // caller key index of every group member, in group order
+  std::vector<uint32_t> group_off;      // G + 1 offsets into key_idx
   std::vector<uint8_t> group_msg;       // G x mlen
-  std::vector<uint8_t> group_dom;       // G x 8 (domain of the owning call)
-  std::vector<int32_t> pair_src;        // >= 0: group index; < 0: -(call + 1) = signature pair
-  std::vector<uint32_t> call_pair_off;  // n_calls + 1 offsets into pairs
-  std::vector<std::vector<agg_chunk>> passes;  // segmented Fp12 product passes
-  AggPlan agg;                                 // group pubkey sums
+  std::vector<uint32_t> group_call;     // G: owning call (whose domain hashes the message)
+  std::vector<int32_t> quad_pair;       // 2 per quad: group >= 0, -(call + 1) = the signature pair, or PAIR_NONE
+  std::vector<uint32_t> call_quad_off;  // n_calls + 1 offsets into the quads
+  std::vector<std::vector<agg_chunk>> passes;  // segmented Fp12 products (empty: one quad per call)
+  AggPlan agg;                                 // group pubkey sums over key_idx order
 };
 
 constexpr uint32_t PROD_CHUNK = 8;
@@ -389,78 +401,119 @@ std::vector<std::vector<agg_chunk>> plan_products(std::vector<uint32_t> off) {
   return passes;
 }
 
-VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* pks, const uint8_t* msgs, size_t mlen,
-               const uint8_t* dom8s, int dom_stride, const int* with_sig) {
+bool is_inf_encoding(const uint8_t* b, size_t len) {
+  if (b[0] != 0xC0) return false;
+  for (size_t i = 1; i < len; ++i)
+    if (b[i]) return false;
+  return true;
+}
+
+// h_pks / h_sigs may be NULL (device-resident keys / signatures: nothing is dropped)
+VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, size_t mlen, const uint8_t* h_pks,
+               const uint8_t* h_sigs, const int* with_sig) {
   VmPlan pl;
   pl.n_calls = n_calls;
+  pl.n_keys = call_off[n_calls];
   pl.group_off.push_back(0);
-  pl.call_pair_off.push_back(0);
+  pl.call_quad_off.push_back(0);
   for (size_t c = 0; c < n_calls; ++c) {
     std::unordered_map<std::string, uint32_t> idx;
     std::vector<std::vector<uint32_t>> members;
+    std::vector<uint32_t> first;
     for (uint32_t i = call_off[c]; i < call_off[c + 1]; ++i) {
       std::string key((const char*)msgs + mlen * i, mlen);
       auto it = idx.find(key);
       if (it == idx.end()) {
         idx.emplace(key, (uint32_t)members.size());
         members.push_back({i});
-        pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * i, msgs + mlen * (i + 1));
-        pl.group_dom.insert(pl.group_dom.end(), dom8s + (size_t)dom_stride * c, dom8s + (size_t)dom_stride * c + 8);
+        first.push_back(i);
       } else {
         members[it->second].push_back(i);
       }
     }
-    for (auto& m : members) {
-      for (uint32_t i : m) pl.pks_perm.insert(pl.pks_perm.end(), pks + 48 * (size_t)i, pks + 48 * ((size_t)i + 1));
-      pl.group_off.push_back((uint32_t)(pl.pks_perm.size() / 48));
-      pl.pair_src.push_back((int32_t)pl.G);
+    std::vector<int32_t> pairs;
+    for (size_t gi = 0; gi < members.size(); ++gi) {
+      const auto& m = members[gi];
+      if (h_pks) {
+        bool all_inf = true;
+        for (uint32_t i : m) all_inf = all_inf && is_inf_encoding(h_pks + 48 * (size_t)i, 48);
+        if (all_inf) continue;
+      }
+      pl.key_idx.insert(pl.key_idx.end(), m.begin(), m.end());
+      pl.group_off.push_back((uint32_t)pl.key_idx.size());
+      pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * first[gi], msgs + mlen * (first[gi] + 1));
+      pl.group_call.push_back((uint32_t)c);
+      pairs.push_back((int32_t)pl.G);
       ++pl.G;
     }
-    if (with_sig[c]) pl.pair_src.push_back(-(int32_t)c - 1);
-    pl.call_pair_off.push_back((uint32_t)pl.pair_src.size());
+    if (with_sig[c] && !(h_sigs && is_inf_encoding(h_sigs + 96 * c, 96))) pairs.push_back(-(int32_t)c - 1);
+    if (pairs.empty()) pairs.push_back(PAIR_NONE);   // the empty product: one idle quad, f = 1
+    for (size_t k = 0; k < pairs.size(); k += 2) {
+      pl.quad_pair.push_back(pairs[k]);
+      pl.quad_pair.push_back(k + 1 < pairs.size() ? pairs[k + 1] : PAIR_NONE);
+    }
+    pl.call_quad_off.push_back((uint32_t)(pl.quad_pair.size() / 2));
   }
-  pl.npairs = pl.pair_src.size();
-  pl.passes = plan_products(pl.call_pair_off);
+  pl.nquads = pl.quad_pair.size() / 2;
+  if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
   if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
   return pl;
 }
 
-// one Miller loop per pair; statuses: any BAD operand -> BAD, an infinite operand -> 1
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_miller_pairs_batch(size_t npairs, const int32_t* __restrict__ src,
-                                                              size_t G, const uint32_t* __restrict__ h_aff,
-                                                              const uint8_t* __restrict__ h_st,
-                                                              const uint32_t* __restrict__ agg_aff,
-                                                              const uint8_t* __restrict__ agg_st, size_t ncalls,
-                                                              const uint32_t* __restrict__ sig_aff,
-                                                              const uint8_t* __restrict__ sig_st,
-                                                              uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t k = item_index<2>();
-  if (k >= npairs) return;
-  const int32_t s = src[k];
-  uint8_t sq, sp;
-  aff_t<fp2p_t> Q;
-  aff_t<fp_t> P;
-  if (s >= 0) {
-    sq = h_st[s];
-    sp = agg_st[s];
-    if (sq == ST_OK && sp == ST_OK) { Q = soa_ld_g2(h_aff, G, (size_t)s); P = soa_ld_g1(agg_aff, G, (size_t)s); }
+// Each lane quad runs (up to) two pairs of one call, one per half (bls381_quad.hpp).
+// A half's pair is idle for PAIR_NONE or an infinite operand (py_ecc: pairing 1);
+// any undecodable / bad operand makes the quad BAD; so does a degenerate loop.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(size_t nq, const int32_t* __restrict__ quad_pair,
+                                                        size_t G, const uint32_t* __restrict__ h_aff,
+                                                        const uint8_t* __restrict__ h_st,
+                                                        const uint32_t* __restrict__ agg_aff,
+                                                        const uint8_t* __restrict__ agg_st, size_t ncalls,
+                                                        const uint32_t* __restrict__ sig_aff,
+                                                        const uint8_t* __restrict__ sig_st,
+                                                        uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t q = item_index<4>();
+  if (q >= nq) return;
+  const bool hi = qd_hi();
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const int p = pr_odd() ? 1 : 0;
+  auto status = [&](int32_t src, bool& bad) -> bool {   // active?
+    uint8_t sq = ST_INF, sp = ST_INF;
+    if (src >= 0) { sq = h_st[src]; sp = agg_st[src]; }
+    else if (src != PAIR_NONE) { sq = sig_st[(size_t)(-src - 1)]; sp = ST_OK; }
+    bad = sq == ST_BAD || sp == ST_BAD;
+    return sq == ST_OK && sp == ST_OK;
+  };
+  const int32_t mine = quad_pair[2 * q + (hi ? 1 : 0)], other = quad_pair[2 * q + (hi ? 0 : 1)];
+  bool bad_m, bad_o;
+  const bool act_m = status(mine, bad_m), act_o = status(other, bad_o);
+  if (bad_m || bad_o) { if (lead) st_out[q] = ST_BAD; return; }   // same on all four lanes
+  fq12_t f;
+  bool degen = false;
+  if (act_m || act_o) {
+    // an idle half runs a copy of the active half's operands with its lines masked to 1
+    const int32_t src = act_m ? mine : other;
+    aff_t<fp2p_t> Q;
+    aff_t<fp_t> P;
+    if (src >= 0) {
+      Q.x = pr_make(soa_ld(h_aff, 2 * G, 2 * (size_t)src + p, 0));
+      Q.y = pr_make(soa_ld(h_aff, 2 * G, 2 * (size_t)src + p, 1));
+      P = soa_ld_g1(agg_aff, G, (size_t)src);
+    } else {
+      const size_t c = (size_t)(-src - 1);
+      Q.x = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 0));
+      Q.y = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 1));
+      P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M;
+    }
+    f = miller_loop_quad(Q, g1_prepare(P), act_m, degen);
   } else {
-    const size_t c = (size_t)(-s - 1);
-    sq = sig_st[c];
-    sp = ST_OK;
-    if (sq == ST_OK) { Q = soa_ld_g2(sig_aff, ncalls, c); P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M; }
+    f = fq12_one();
   }
-  fp12p_t f = fp12_one<fp2p_t>();
-  uint8_t st = ST_OK;
-  if (sq == ST_BAD || sp == ST_BAD) {
-    st = ST_BAD;
-  } else if (sq == ST_OK && sp == ST_OK) {
-    bool degen = false;
-    f = miller_loop_1(Q, g1_prepare(P), degen);
-    if (degen) st = ST_BAD;   // py_ecc's zero pairing value (miller_loop_n)
-  }
-  soa_st12(f_out, npairs, k, f);
-  if (!pr_odd()) st_out[k] = st;
+  const size_t lp = 2 * q + p;
+  const int c0 = hi ? 3 : 0;
+  soa_st(f_out, 2 * nq, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * nq, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * nq, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[q] = degen ? ST_BAD : ST_OK;
 }
 
 // each lane multiplies one chunk [begin, end) of Fp12 values (statuses OR-ed);
@@ -482,64 +535,84 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_chunk_product
   if (!pr_odd()) out_st[c] = st;
 }
 
-// Runs a planned batch up to (and excluding) the final exponentiation.  Returns
-// per-call Fp12 products and statuses (SoA over n_calls) on the device.
-int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bump& b, hipStream_t s,
-                 uint32_t** out_f, uint8_t** out_st) {
-  const size_t G = pl.G, ncalls = pl.n_calls, np = pl.npairs;
-  uint8_t* d_pks = b.take<uint8_t>(pl.pks_perm.size() + 1);
-  uint8_t* d_msgs = b.take<uint8_t>(pl.group_msg.size() + 1);
-  uint8_t* d_doms = b.take<uint8_t>(pl.group_dom.size() + 1);
-  uint8_t* d_sigs = b.take<uint8_t>(96 * ncalls);
-  int32_t* d_src = b.take<int32_t>(np + 1);
-  if (!pl.pks_perm.empty()) HIPC(hipMemcpyAsync(d_pks, pl.pks_perm.data(), pl.pks_perm.size(), hipMemcpyHostToDevice, s));
-  if (!pl.group_msg.empty()) HIPC(hipMemcpyAsync(d_msgs, pl.group_msg.data(), pl.group_msg.size(), hipMemcpyHostToDevice, s));
-  if (!pl.group_dom.empty()) HIPC(hipMemcpyAsync(d_doms, pl.group_dom.data(), pl.group_dom.size(), hipMemcpyHostToDevice, s));
-  HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * ncalls, hipMemcpyHostToDevice, s));
-  if (np) HIPC(hipMemcpyAsync(d_src, pl.pair_src.data(), np * sizeof(int32_t), hipMemcpyHostToDevice, s));
-  // Small batches (an epoch's attestations, one custody call) leave most of the
-  // GPU idle, so the independent stages overlap: the pubkey-group sums and the
-  // signature decodes run on the side stream while the main stream hashes the
-  // messages; the Miller loops wait for both.
+// rows idx[k] of `src` (row_bytes each) -> dst row k
+__global__ void __launch_bounds__(KBLOCK) k_gather_rows(size_t n, const uint32_t* __restrict__ idx,
+                                                        const uint8_t* __restrict__ src, uint32_t row_bytes,
+                                                        uint8_t* __restrict__ dst) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * row_bytes) return;
+  const size_t k = t / row_bytes, b = t % row_bytes;
+  dst[t] = src[(size_t)idx[k] * row_bytes + b];
+}
+
+// Runs a planned batch up to (and excluding) the final exponentiation: keys,
+// signatures and domains are device buffers (d_pks indexed by the caller's key
+// numbering); the plan's own arrays are copied here.  Returns per-call Fp12
+// products and statuses (SoA over n_calls) on the device.
+int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, const uint8_t* d_sigs,
+                 const uint8_t* d_doms, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st) {
+  const size_t G = pl.G, ncalls = pl.n_calls, nq = pl.nquads;
+  const int chk = check_subgroups();   // STRICT: every member key and signature is checked
+  uint32_t* d_kidx = b.take<uint32_t>(pl.key_idx.size() + 1);
+  uint8_t* d_gmsg = b.take<uint8_t>(pl.group_msg.size() + 1);
+  uint32_t* d_gcall = b.take<uint32_t>(G + 1);
+  uint8_t* d_gdom = b.take<uint8_t>(8 * G + 1);
+  uint8_t* d_gpks = b.take<uint8_t>(48 * pl.key_idx.size() + 1);
+  int32_t* d_qp = b.take<int32_t>(2 * nq);
+  if (!pl.key_idx.empty())
+    HIPC(hipMemcpyAsync(d_kidx, pl.key_idx.data(), 4 * pl.key_idx.size(), hipMemcpyHostToDevice, s));
+  if (G) {
+    HIPC(hipMemcpyAsync(d_gmsg, pl.group_msg.data(), pl.group_msg.size(), hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(d_gcall, pl.group_call.data(), 4 * G, hipMemcpyHostToDevice, s));
+  }
+  HIPC(hipMemcpyAsync(d_qp, pl.quad_pair.data(), 8 * nq, hipMemcpyHostToDevice, s));
   uint32_t* agg_aff = b.take<uint32_t>(2 * FP_LIMBS * (G + 1));
   uint8_t* agg_st = b.take<uint8_t>(G + 1);
   uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
   uint8_t* h_st = b.take<uint8_t>(G + 1);
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
-  const int chk = check_subgroups();   // STRICT: every member key and signature is checked
+  // Small batches (an epoch's attestations, one custody call) leave most of the
+  // GPU idle, so the independent stages overlap: the pubkey-group sums and the
+  // signature decodes run on the side stream while the main stream hashes the
+  // messages; the Miller loops wait for both.
   {
     std::lock_guard<std::mutex> fk(c->fork_mu);
     hipStream_t side = c->side;
     HIPC(hipEventRecord(c->ev_fork, s));
     HIPC(hipStreamWaitEvent(side, c->ev_fork, 0));
     if (G > 0) {
-      // group sums -> affine + subgroup check
+      // members in group order, then group sums -> affine
+      const size_t nk = pl.key_idx.size();
+      if (nk) LAUNCH("gather_pubkeys", side, dim3(grid_for(48 * nk)), dim3(KBLOCK), k_gather_rows, nk,
+                     (const uint32_t*)d_kidx, d_pks, 48u, d_gpks);
       const uint32_t* jac;
       const uint8_t* bad;
       size_t used = 0;
       uint8_t* sub = b.take<uint8_t>(0);
-      int rc = run_agg<fp_t>(pl.agg, G, d_pks, sub, side, &jac, &bad, &used, b.left(), nullptr, chk);
+      int rc = run_agg<fp_t>(pl.agg, G, d_gpks, sub, side, &jac, &bad, &used, b.left(), nullptr, chk);
       if (rc) return rc;
       b.off += used;
       LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
     }
-    LAUNCH("decode_g2", side, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, (const uint8_t*)d_sigs,
-           sig_aff, sig_st, chk);
+    LAUNCH("decode_g2", side, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, d_sigs, sig_aff, sig_st,
+           chk);
     HIPC(hipEventRecord(c->ev_join, side));
-    if (G > 0)
-      LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_msgs,
-             (uint32_t)mlen, (const uint8_t*)d_doms, 8, h_aff, h_st);
+    if (G > 0) {
+      LAUNCH("gather_domains", s, dim3(grid_for(8 * G)), dim3(KBLOCK), k_gather_rows, G, (const uint32_t*)d_gcall,
+             d_doms, 8u, d_gdom);
+      LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
+             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st);
+    }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   }
-  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * (np + 1));
-  uint8_t* st = b.take<uint8_t>(np + 1);
-  if (np)
-    LAUNCH("miller_loop_1", s, dim3(grid_for(2 * np)), dim3(KBLOCK), k_miller_pairs_batch, np, (const int32_t*)d_src, G,
-           (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
-           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nq);
+  uint8_t* st = b.take<uint8_t>(nq);
+  LAUNCH("miller_quads", s, dim3(grid_for(4 * nq)), dim3(KBLOCK), k_miller_quads, nq, (const int32_t*)d_qp, G,
+         (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+         (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
   // segmented products (chunk lists live in the plan, which outlives the stream work)
-  size_t n_in = np;
+  size_t n_in = nq;
   for (const auto& chunks : pl.passes) {
     agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
     uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
@@ -556,17 +629,37 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* sigs, Bum
   return 0;
 }
 
+// workspace bound of run_vm_batch for a plan (plus the final verdict bytes)
 size_t vm_ws_bound(const VmPlan& pl, size_t mlen) {
-  const size_t G = pl.G + 1, np = pl.npairs + 1, nc = pl.n_calls + 1;
+  const size_t G = pl.G + 1, nq = pl.nquads + 1, nc = pl.n_calls + 1, nk = pl.key_idx.size() + 1;
   size_t s = 1 << 16;
-  s += align256(pl.pks_perm.size() + 1) + align256(G * mlen + 1) + align256(G * 8 + 1) + align256(96 * nc) +
-       align256(4 * np);
+  s += align256(4 * nk) + align256(G * mlen + 1) + align256(4 * G) + align256(8 * G + 1) + align256(48 * nk) +
+       align256(8 * nq);
   s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
   s += agg_ws_size(pl.agg, 3) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
-  s += align256(12 * FPW * np) + align256(np);
+  s += align256(12 * FPW * nq) + align256(nq);
   for (const auto& ch : pl.passes)
     s += align256(ch.size() * sizeof(agg_chunk)) + align256(12 * FPW * ch.size()) + align256(ch.size());
+  s += align256(nc);
+  return s;
+}
+
+// the same bound from sizes alone (device entry point: the caller sizes the workspace before the plan exists)
+size_t vm_ws_bound_sizes(size_t n_calls, size_t n_keys, size_t mlen) {
+  const size_t G = n_keys + 1, nq = n_keys / 2 + n_calls + 1, nc = n_calls + 1, nk = n_keys + 1;
+  size_t s = 1 << 16;
+  s += align256(4 * nk) + align256(G * mlen + 1) + align256(4 * G) + align256(8 * G + 1) + align256(48 * nk) +
+       align256(8 * nq);
+  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
+  // group-sum levels: chunks <= groups + keys / CHUNK per level, three levels at most below 2^27 keys
+  const size_t chunks = G + n_keys / CHUNK_L1 + 1;
+  s += 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks)) + 256;
+  s += align256(4 * FPW * nc) + align256(nc);
+  s += align256(12 * FPW * nq) + align256(nq);
+  // product passes: <= nq / 8 + n_calls chunks per pass, and the sizes shrink 8x per pass
+  const size_t pc = nq / 4 + 2 * nc;
+  s += 8 * (align256(pc * sizeof(agg_chunk)) + align256(12 * FPW * pc) + align256(pc));
   s += align256(nc);
   return s;
 }
@@ -716,6 +809,28 @@ int bls381_verify(const uint8_t pk[48], const uint8_t* msg, size_t msg_len, cons
   return bls381_verify_multiple(1, pk, msg, msg_len, sig, dom8);
 }
 
+// host buffers -> device copies -> the planned pipeline (keys dropped from the plan when all-infinite)
+static int vm_host(Ctx* c, size_t n_calls, const uint32_t* call_off, const uint8_t* pks, const uint8_t* msgs,
+                   size_t msg_len, const uint8_t* sigs, const uint8_t* dom8s, const int* with_sig, Bump& b,
+                   uint32_t** f, uint8_t** st) {
+  const size_t nk = call_off[n_calls];
+  auto pl = std::make_shared<VmPlan>(plan_vm(n_calls, call_off, msgs, msg_len, pks, sigs, with_sig));
+  int rc;
+  if ((rc = ensure_ws(c, vm_ws_bound(*pl, msg_len) + align256(48 * nk + 1) + align256(96 * n_calls) +
+                             align256(8 * n_calls) + 4096)))
+    return rc;
+  b = Bump(c->ws, c->ws_cap);
+  uint8_t* d_pks = b.take<uint8_t>(48 * nk + 1);
+  uint8_t* d_sigs = b.take<uint8_t>(96 * n_calls);
+  uint8_t* d_doms = b.take<uint8_t>(8 * n_calls);
+  hipStream_t s = c->stream;
+  if (nk) HIPC(hipMemcpyAsync(d_pks, pks, 48 * nk, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * n_calls, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n_calls, hipMemcpyHostToDevice, s));
+  if ((rc = run_vm_batch(c, *pl, msg_len, d_pks, d_sigs, d_doms, b, s, f, st))) return rc;
+  return keep_until_done(c, s, pl);   // the plan's arrays are async copy sources
+}
+
 int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
                                  const uint8_t* msgs, size_t msg_len, const uint8_t* sigs, const uint8_t* dom8s,
                                  uint8_t* verdicts) try {
@@ -727,18 +842,48 @@ int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(c->mu);
   std::vector<int> with_sig(n_calls, 1);
-  VmPlan pl = plan_vm(n_calls, call_off, pks, msgs, msg_len, dom8s, 8, with_sig.data());
-  if ((rc = ensure_ws(c, vm_ws_bound(pl, msg_len)))) return rc;
-  Bump b(c->ws, c->ws_cap);
+  Bump b(nullptr, 0);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = run_vm_batch(c, pl, msg_len, sigs, b, c->stream, &f, &st))) return rc;
+  if ((rc = vm_host(c, n_calls, call_off, pks, msgs, msg_len, sigs, dom8s, with_sig.data(), b, &f, &st))) return rc;
   uint8_t* d_v = b.take<uint8_t>(n_calls);
   LAUNCH("final_exp", c->stream, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
          (const uint32_t*)f, (const uint8_t*)st, d_v);
   HIPC(hipMemcpyAsync(verdicts, d_v, n_calls, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+size_t bls381_verify_multiple_batch_workspace_size(size_t n_calls, size_t n_pks, size_t msg_len) {
+  return vm_ws_bound_sizes(n_calls, n_pks, msg_len) + align256(n_calls) + 4096;
+}
+
+int bls381_verify_multiple_batch_device(size_t n_calls, const uint32_t* h_call_off, const uint8_t* h_msgs,
+                                        size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                        const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                        void* stream) try {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n_calls == 0) return 0;
+  if (!h_call_off || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  const size_t nk = h_call_off[n_calls];
+  if (h_call_off[0] != 0 || (nk && (!d_pks || (!h_msgs && msg_len)))) return BLS381_EARG;
+  for (size_t k = 0; k < n_calls; ++k)
+    if (h_call_off[k + 1] < h_call_off[k]) return BLS381_EARG;
+  std::vector<int> with_sig(n_calls, 1);
+  auto pl = std::make_shared<VmPlan>(plan_vm(n_calls, h_call_off, h_msgs, msg_len, nullptr, nullptr, with_sig.data()));
+  hipStream_t s = (hipStream_t)stream;
+  Bump b(d_workspace, bls381_verify_multiple_batch_workspace_size(n_calls, nk, msg_len));
+  uint32_t* f;
+  uint8_t* st;
+  if ((rc = run_vm_batch(c, *pl, msg_len, d_pks, d_sigs, d_dom8s, b, s, &f, &st))) return rc;
+  LAUNCH("final_exp", s, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls, (const uint32_t*)f,
+         (const uint8_t*)st, d_verdicts);
+  return keep_until_done(c, s, pl);   // the plan's arrays are async copy sources
 } catch (const std::exception& e) {
   t_err = e.what();
   return BLS381_EARG;
@@ -762,12 +907,10 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
   std::lock_guard<std::mutex> lk(c->mu);
   const uint32_t off[2] = {0, (uint32_t)n};
   const int with_sig = include_sig ? 1 : 0;
-  VmPlan pl = plan_vm(1, off, pks, msgs, msg_len, dom8, 8, &with_sig);
-  if ((rc = ensure_ws(c, vm_ws_bound(pl, msg_len)))) return rc;
-  Bump b(c->ws, c->ws_cap);
+  Bump b(nullptr, 0);
   uint32_t* f;
   uint8_t* st;
-  if ((rc = run_vm_batch(c, pl, msg_len, sig, b, c->stream, &f, &st))) return rc;
+  if ((rc = vm_host(c, 1, off, pks, msgs, msg_len, sig, dom8, &with_sig, b, &f, &st))) return rc;
   uint8_t* d_out = b.take<uint8_t>(576);
   LAUNCH("fp12_to_bytes", c->stream, dim3(1), dim3(KBLOCK), k_fp12_to_bytes, (size_t)1, (const uint32_t*)f, d_out);
   uint8_t h_st = 0;

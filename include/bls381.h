@@ -142,6 +142,19 @@ int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const
                                  const uint8_t* msgs, size_t msg_len, const uint8_t* sigs, const uint8_t* dom8s,
                                  uint8_t* verdicts);
 
+/* Device-resident form (C3: the committee aggregates never leave HBM).  Pubkeys
+ * (d_pks, 48 B each, numbered like the messages), signatures (d_sigs, 96 B per
+ * call) and domains (d_dom8s) are device memory; the call offsets and the
+ * messages stay on the HOST (h_call_off, h_msgs): they decide the per-message
+ * grouping plan, and the messages are copied with it.  d_verdicts[c] = 1/0.  Work
+ * is queued on `stream` (hipStream_t; NULL = the null stream), not synchronised.
+ * The workspace must hold bls381_verify_multiple_batch_workspace_size bytes. */
+size_t bls381_verify_multiple_batch_workspace_size(size_t n_calls, size_t n_pks, size_t msg_len);
+int bls381_verify_multiple_batch_device(size_t n_calls, const uint32_t* h_call_off, const uint8_t* h_msgs,
+                                        size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                        const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                        void* stream);
+
 /* ---- multi-GPU partial products --------------------------- */
 /* Miller-loop product of one shard of a bls_verify_multiple call: pairs
  * (hash_to_G2(msg_g), group_pubkey_g) for the messages in this shard, plus

@@ -704,3 +704,36 @@ def test_c5_verify_multiple_4096_messages(native):
     rc0, a = native.miller_partial(pks[:48 * 2048], b"".join(msgs[:2048]), 32, sig, True, d8)
     rc1, b = native.miller_partial(pks[48 * 2048:], b"".join(msgs[2048:]), 32, sig, False, d8)
     assert rc0 == 0 and rc1 == 0 and native.final_verify(a + b) is True
+
+
+def test_verify_multiple_batch_device_entry(native, golden, torsion):
+    """bls381_verify_multiple_batch_device (keys, signatures, domains in HBM; plan from host
+    offsets + messages): golden and torsion calls in one batch, verdicts == oracle columns."""
+    import ctypes
+    import torch
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    _, gb = golden
+    cases = [(c, c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+    cases += [(c, c["expected_pyecc"]) for c in torsion["verify_multiple"]]
+    off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+    for c, _ in cases:
+        pks += b"".join(bytes.fromhex(p) for p in c["pubkeys"])
+        msgs += b"".join(bytes.fromhex(m) for m in c["messages"])
+        sigs += bytes.fromhex(c["signature"])
+        doms += int(c["domain"]).to_bytes(8, "big")
+        off.append(off[-1] + len(c["pubkeys"]))
+    off = np.array(off, dtype=np.uint32)
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    d_pks, d_sigs, d_doms = t(pks), t(sigs), t(doms)
+    d_v = torch.full((len(cases),), 7, dtype=torch.uint8, device=dev)
+    ws = torch.empty(L.bls381_verify_multiple_batch_workspace_size(len(cases), len(pks) // 48, 32),
+                     dtype=torch.uint8, device=dev)
+    native.set_subgroup_policy("pyecc")
+    native.check(L.bls381_verify_multiple_batch_device(
+        len(cases), off.ctypes.data_as(ctypes.c_void_p), msgs, 32, d_pks.data_ptr(), d_sigs.data_ptr(),
+        d_doms.data_ptr(), d_v.data_ptr(), ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+    del off, msgs                                   # the plan is the engine's own copy
+    got = d_v.cpu().tolist()
+    assert got == [int(e) for _, e in cases]
