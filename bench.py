@@ -484,6 +484,93 @@ def bench_c5(native, args, world, rank, dist, dev):
             "batched": batched}
 
 
+def bench_native_comm(native, args, world, rank, dist, dev):
+    """The library's own RCCL communicator (bls381_amd.comm, no torch in the data path; torch only
+    hands the 128-byte unique id around here): C4 as ONE collective bls_aggregate_pubkeys over all
+    ranks' keys, and one C5 bls_verify_multiple (L = 4096) split across the ranks by message with a
+    single final exponentiation on rank 0."""
+    import torch
+    from bls381_amd import comm
+    if world > 1:
+        box = [comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        uid = box[0]
+    else:
+        uid = comm.unique_id()
+    comm.init(world, rank, uid)
+    out = {"n_gpus": world}
+    try:
+        k = args.c4_keys * world
+        base = native.privtopub_batch(b"".join(j.to_bytes(32, "big") for j in range(1, 65)))
+        keys = np.frombuffer(base, dtype=np.uint8).reshape(64, 48)[np.arange(k) % 64]
+        key_list = [bytes(r) for r in keys]
+        want = native.privtopub_batch((sum((i % 64) + 1 for i in range(k)) % R_ORDER).to_bytes(32, "big"))
+        assert comm.aggregate_pubkeys(key_list) == want, "native C4 aggregate mismatch"
+        steps = max(args.steps, 3)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            comm.aggregate_pubkeys(key_list)
+        t = _max_time(time.perf_counter() - t0, world, dist, dev)
+        out["c4_aggregate"] = {"pubkeys": k, "pubkeys_aggregated_per_s": k * steps / t, "ms_per_aggregate": 1e3 * t / steps,
+                               "note": "host keys in (PCIe copies inside the time), one collective call"}
+        rng = np.random.default_rng(0xB15_0005)
+        Lm = 4096
+        sks = [int.from_bytes(rng.bytes(32), "big") % (R_ORDER - 1) + 1 for _ in range(Lm)]
+        skb = b"".join(x.to_bytes(32, "big") for x in sks)
+        m = rng.bytes(32 * Lm)
+        pkb = native.privtopub_batch(skb)
+        sig = native.aggregate_signatures(native.sign_batch(m, skb, (1).to_bytes(8, "big") * Lm))
+        pk_list = [pkb[48 * j:48 * j + 48] for j in range(Lm)]
+        m_list = [m[32 * j:32 * j + 32] for j in range(Lm)]
+        assert comm.verify_multiple(pk_list, m_list, sig, 1) is True
+        assert comm.verify_multiple(pk_list, m_list, sig, 2) is False
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            comm.verify_multiple(pk_list, m_list, sig, 1)
+        t = _max_time(time.perf_counter() - t0, world, dist, dev)
+        out["c5_split_call"] = {"L": Lm, "ms_per_call": 1e3 * t / steps, "pairings_per_s": (Lm + 1) * steps / t}
+    finally:
+        comm.destroy()
+    return out
+
+
+def bench_latency(native, pks, msgs, sigs, expected):
+    """Single-call latency through the drop-in shim (the reference calls BLS one signature at a
+    time: 0_beacon-chain.md:1594,1603,1664,1756,1796,1824): bls_verify and an attestation-shaped
+    bls_verify_multiple, host bytes in, bool out (PCIe copies, launches and the sync included);
+    plus small device batches, where the quad Miller loop halves the per-item latency."""
+    from bls381_amd import bls
+    reps = 15
+    out = {}
+    times = []
+    for i in range(reps):
+        t0 = time.perf_counter()
+        v = bls.bls_verify(pks[48 * i:48 * i + 48], msgs[32 * i:32 * i + 32], sigs[96 * i:96 * i + 96], DOMAIN_DEPOSIT)
+        times.append(time.perf_counter() - t0)
+        assert v == bool(expected[i])
+    out["bls_verify_ms"] = {"median": 1e3 * float(np.median(times)), "min": 1e3 * min(times)}
+    inf = bytes([0xC0]) + bytes(47)
+    times = []
+    for i in range(reps):
+        t0 = time.perf_counter()
+        bls.bls_verify_multiple([pks[48 * i:48 * i + 48], inf], [msgs[32 * i:32 * i + 32], bytes(32)],
+                                sigs[96 * i:96 * i + 96], DOMAIN_DEPOSIT)
+        times.append(time.perf_counter() - t0)
+    out["bls_verify_multiple_attestation_ms"] = {"median": 1e3 * float(np.median(times)), "min": 1e3 * min(times)}
+    for k in (64, 1024, 16384):
+        native.verify_batch(pks[:48 * k], msgs[:32 * k], sigs[:96 * k], DOMAIN_DEPOSIT.to_bytes(8, "big") * k)
+        t0 = time.perf_counter()
+        v = native.verify_batch(pks[:48 * k], msgs[:32 * k], sigs[:96 * k], DOMAIN_DEPOSIT.to_bytes(8, "big") * k)
+        dt = time.perf_counter() - t0
+        assert np.array_equal(v, expected[:k])
+        out["verify_batch_%d" % k] = {"ms": 1e3 * dt, "verifications_per_s": k / dt}
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -609,6 +696,9 @@ def main():
         sec["c3_epoch"] = bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist)
         sec["c4_aggregate"] = bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist)
         sec["c5_multi_pairing"] = bench_c5(native, args, world, rank, dist, dev)
+        sec["native_rccl"] = bench_native_comm(native, args, world, rank, dist, dev)
+        if rank == 0:
+            sec["latency"] = bench_latency(native, pks, msgs, sigs, expected)
 
     if rank != 0:
         if world > 1:

@@ -59,6 +59,16 @@ _SIGS = {
     "bls381_miller_partial": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int,
                                              _u8p, _u8p]),
     "bls381_final_verify": (ctypes.c_int, [ctypes.c_size_t, _u8p]),
+    "bls381_comm_unique_id": (ctypes.c_int, [_u8p]),
+    "bls381_comm_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u8p]),
+    "bls381_comm_init_virtual": (ctypes.c_int, [ctypes.c_int]),
+    "bls381_comm_size": (ctypes.c_int, []),
+    "bls381_comm_rank": (ctypes.c_int, []),
+    "bls381_comm_destroy": (None, []),
+    "bls381_verify_multiple_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_aggregate_pubkeys_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_verify_multiple_batch_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, ctypes.c_size_t,
+                                                            _u8p, _u8p, _u8p]),
     "bls381_ssz_root_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, ctypes.c_uint32, _u8p]),
     "bls381_ssz_root_workspace_size": (ctypes.c_size_t, []),
     "bls381_ssz_root_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, ctypes.c_size_t, _u8p,

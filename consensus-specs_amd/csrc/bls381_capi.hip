@@ -4,7 +4,9 @@
 // launch pipelines for each entry point, HIP-event kernel accounting for
 // bench.py.  No CPU fallback: without a gfx950 device every entry point
 // returns BLS381_ENODEV.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <atomic>
 #include <cstdio>
@@ -1559,6 +1561,370 @@ int bls381_verify_deposits(size_t n, const uint8_t* deposit_data, const uint8_t*
   if ((rc = bls381_verify_deposits_device(n, d_dd, d_dom, d_ver, d_ws, s))) return rc;
   HIPC(hipMemcpyAsync(verdicts, d_ver, n, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+}  // extern "C"
+
+// ---- multi-GPU over RCCL: one process per GPU, a communicator
+// inside the library.  RCCL is opened with dlopen when a communicator is first
+// made, so the library itself does not depend on it.
+namespace {
+
+struct RcclApi {
+  void* h = nullptr;
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+RcclApi* rccl_api() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so"}) {
+      api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+      if (api.h) break;
+    }
+    if (!api.h) return;
+    api.get_unique_id = (decltype(api.get_unique_id))dlsym(api.h, "ncclGetUniqueId");
+    api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(api.h, "ncclCommInitRank");
+    api.comm_destroy = (decltype(api.comm_destroy))dlsym(api.h, "ncclCommDestroy");
+    api.all_gather = (decltype(api.all_gather))dlsym(api.h, "ncclAllGather");
+    api.broadcast = (decltype(api.broadcast))dlsym(api.h, "ncclBroadcast");
+    api.error_string = (decltype(api.error_string))dlsym(api.h, "ncclGetErrorString");
+  });
+  if (!api.h || !api.get_unique_id || !api.comm_init_rank || !api.comm_destroy || !api.all_gather ||
+      !api.broadcast || !api.error_string) {
+    t_err = "RCCL (librccl.so) not loadable";
+    return nullptr;
+  }
+  return &api;
+}
+
+// A communicator is RCCL's (one rank per process), or "virtual": one process
+// plays all nranks ranks on its own GPU (the partition, per-rank partials and
+// the rank-0 combination run unchanged; the all-gather is a device copy).
+// RCCL refuses two ranks on one GPU, so the virtual form is how the sharded
+// protocol is exercised with several ranks on a one-GPU box.
+struct Comm {
+  ncclComm_t comm = nullptr;
+  bool virt = false;
+  int nranks = 0, rank = -1, device = -1;
+  uint8_t* rows = nullptr;   // gathered per-rank rows (device), grown on demand
+  size_t rows_cap = 0;
+};
+std::mutex g_comm_mu;
+Comm g_comm;
+
+int nccl_fail(RcclApi* api, const char* what, ncclResult_t r) {
+  t_err = std::string(what) + ": " + api->error_string(r);
+  return BLS381_EHIP;
+}
+#define NCCLC(api, x)                                            \
+  do {                                                           \
+    ncclResult_t r__ = (x);                                      \
+    if (r__ != ncclSuccess) return nccl_fail(api, #x, r__);      \
+  } while (0)
+
+// Fp12 value (SoA, one item) -> 576 canonical bytes, or 576 zero bytes when its
+// status is not OK (an honest partial product is never 0; a zero row makes the
+// gathered product 0 and the verdict False on rank 0)
+__global__ void __launch_bounds__(KBLOCK) k_fp12_row(const uint32_t* __restrict__ f, const uint8_t* __restrict__ st,
+                                                     uint8_t* __restrict__ out576) {
+  if (threadIdx.x >= 2) return;
+  const int p = pr_odd() ? 1 : 0;
+  const bool ok = st[0] == ST_OK;
+  const fp12p_t a = soa_ld12(f, 1, 0);
+  const fp2p_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
+  for (int k = 0; k < 6; ++k) {
+    uint8_t* o = out576 + 96 * k + 48 * p;
+    if (ok) fp_plain_to_be48(o, fp_from_mont(cs[k]->v));
+    else for (int b = 0; b < 48; ++b) o[b] = 0;
+  }
+}
+
+// compressed partial aggregate, or 48 zero bytes (not a valid encoding) when its status is an error
+__global__ void __launch_bounds__(KBLOCK) k_zero_if_error(const int32_t* __restrict__ st, uint8_t* __restrict__ buf,
+                                                          uint32_t len) {
+  const uint32_t t = threadIdx.x;
+  if (t < len && st[0] != 0) buf[t] = 0;
+}
+
+Comm* comm_ctx(int* rc) {
+  if (!g_comm.comm && !g_comm.virt) {
+    t_err = "no communicator: call bls381_comm_init first";
+    *rc = BLS381_EARG;
+    return nullptr;
+  }
+  return &g_comm;
+}
+
+int comm_rows(Comm* cm, size_t bytes, uint8_t** out) {
+  if (cm->rows_cap < bytes) {
+    if (cm->rows) HIPC(hipFree(cm->rows));
+    cm->rows = nullptr;
+    cm->rows_cap = 0;
+    HIPC(hipMalloc(&cm->rows, bytes));
+    cm->rows_cap = bytes;
+  }
+  *out = cm->rows;
+  return 0;
+}
+
+// the ranks whose rows this process computes: its own, or all of them (virtual)
+int first_rank(const Comm* cm) { return cm->virt ? 0 : cm->rank; }
+int last_rank(const Comm* cm) { return cm->virt ? cm->nranks - 1 : cm->rank; }
+bool is_root(const Comm* cm) { return cm->virt || cm->rank == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int bls381_comm_unique_id(uint8_t out[128]) {
+  if (!out) return BLS381_EARG;
+  RcclApi* api = rccl_api();
+  if (!api) return BLS381_ENODEV;
+  ncclUniqueId id;
+  NCCLC(api, api->get_unique_id(&id));
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+int bls381_comm_init(int nranks, int rank, const uint8_t uid[128]) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || !uid) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);   // this thread's device (bls381_init) is the rank's GPU
+  if (!c) return rc;
+  RcclApi* api = rccl_api();
+  if (!api) return BLS381_ENODEV;
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  if (g_comm.comm || g_comm.virt) { t_err = "communicator already initialised"; return BLS381_EARG; }
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof(id));
+  ncclComm_t comm;
+  NCCLC(api, api->comm_init_rank(&comm, nranks, id, rank));
+  g_comm.comm = comm;
+  g_comm.nranks = nranks;
+  g_comm.rank = rank;
+  g_comm.device = c->device;
+  return 0;
+}
+
+int bls381_comm_init_virtual(int nranks) {
+  if (nranks < 1) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  if (g_comm.comm || g_comm.virt) { t_err = "communicator already initialised"; return BLS381_EARG; }
+  g_comm.virt = true;
+  g_comm.nranks = nranks;
+  g_comm.rank = 0;
+  g_comm.device = c->device;
+  return 0;
+}
+
+int bls381_comm_size(void) { return (g_comm.comm || g_comm.virt) ? g_comm.nranks : 0; }
+int bls381_comm_rank(void) { return (g_comm.comm || g_comm.virt) ? g_comm.rank : -1; }
+
+void bls381_comm_destroy(void) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  if (g_comm.comm) {
+    RcclApi* api = rccl_api();
+    if (api) (void)api->comm_destroy(g_comm.comm);
+  }
+  if (g_comm.rows) {
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_comm.rows);
+  }
+  g_comm = Comm();
+}
+
+int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len,
+                                   const uint8_t sig[96], const uint8_t dom8[8]) try {
+  if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  Comm* cm = comm_ctx(&rc);
+  if (!cm) return rc;
+  RcclApi* api = cm->virt ? nullptr : rccl_api();
+  if (!cm->virt && !api) return BLS381_ENODEV;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t R = (size_t)cm->nranks;
+  hipStream_t s = c->stream;
+  uint8_t* d_rows;
+  if ((rc = comm_rows(cm, 576 * R + 576, &d_rows))) return rc;
+  // distinct message k (first-appearance order) -> rank k mod nranks: a message's
+  // pubkey group never straddles two ranks (bls381_amd/sharding.py partition_messages)
+  std::unordered_map<std::string, uint32_t> order;
+  std::vector<uint32_t> owner(n);
+  for (size_t i = 0; i < n; ++i) {
+    std::string key((const char*)msgs + msg_len * i, msg_len);
+    auto it = order.find(key);
+    if (it == order.end()) it = order.emplace(key, (uint32_t)order.size()).first;
+    owner[i] = it->second % (uint32_t)R;
+  }
+  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
+    std::vector<uint8_t> my_pks, my_msgs;
+    for (size_t i = 0; i < n; ++i) {
+      if ((int)owner[i] != r) continue;
+      my_pks.insert(my_pks.end(), pks + 48 * i, pks + 48 * (i + 1));
+      my_msgs.insert(my_msgs.end(), msgs + msg_len * i, msgs + msg_len * (i + 1));
+    }
+    const uint32_t off[2] = {0, (uint32_t)(my_pks.size() / 48)};
+    const int with_sig = r == 0 ? 1 : 0;
+    Bump b(nullptr, 0);
+    uint32_t* f;
+    uint8_t* st;
+    if ((rc = vm_host(c, 1, off, my_pks.data(), my_msgs.data(), msg_len, sig, dom8, &with_sig, b, &f, &st)))
+      return rc;
+    // this rank's row (576 B, zero when a member is invalid): in place when virtual
+    uint8_t* row = cm->virt ? d_rows + 576 * (size_t)r : d_rows + 576 * R;
+    LAUNCH("fp12_row", s, dim3(1), dim3(KBLOCK), k_fp12_row, (const uint32_t*)f, (const uint8_t*)st, row);
+    HIPC(hipStreamSynchronize(s));   // the next rank's plan reuses the workspace
+  }
+  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 576 * R, d_rows, 576, ncclUint8, cm->comm, s));
+  if ((rc = ensure_ws(c, 12 * FPW * R * 4 + 4 * R + 65536))) return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_v = b.take<uint8_t>(1);
+  if (is_root(cm)) {   // one final exponentiation, on rank 0
+    uint32_t* g = b.take<uint32_t>(12 * FP_LIMBS * R);
+    uint8_t* gst = b.take<uint8_t>(R);
+    HIPC(hipMemsetAsync(gst, ST_OK, R, s));
+    LAUNCH("fp12_from_bytes", s, dim3(grid_for(2 * R)), dim3(KBLOCK), k_fp12_from_bytes, R, (const uint8_t*)d_rows, g);
+    auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products({0u, (uint32_t)R}));
+    size_t n_in = R;
+    for (const auto& chunks : *passes) {
+      agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
+      uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
+      uint8_t* nst = b.take<uint8_t>(chunks.size());
+      HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+      LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
+             (const agg_chunk*)d_ch, (const uint32_t*)g, n_in, (const uint8_t*)gst, nf, nst);
+      g = nf;
+      gst = nst;
+      n_in = chunks.size();
+    }
+    LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)g,
+           (const uint8_t*)gst, d_v);
+    if ((rc = keep_until_done(c, s, passes))) return rc;
+  }
+  if (!cm->virt) NCCLC(api, api->broadcast(d_v, d_v, 1, ncclUint8, 0, cm->comm, s));
+  uint8_t v = 0;
+  HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return v ? 1 : 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]) try {
+  if (!out || (n && !pks)) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  Comm* cm = comm_ctx(&rc);
+  if (!cm) return rc;
+  RcclApi* api = cm->virt ? nullptr : rccl_api();
+  if (!cm->virt && !api) return BLS381_ENODEV;
+  const size_t R = (size_t)cm->nranks;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipStream_t s = c->stream;
+  uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
+  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;
+  uint8_t* d_sum = d_rows + 48 * R + 48;
+  int32_t* d_st = (int32_t*)(d_sum + 64);
+  // contiguous ranges, sizes differing by at most one (sharding.shard_range)
+  const size_t base = n / R, extra = n % R;
+  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
+    const size_t rr = (size_t)r;
+    const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
+    const uint32_t off1[2] = {0, (uint32_t)cnt};
+    const size_t ws1 = agg_ws_bytes(0, 1, off1);
+    if ((rc = ensure_ws(c, align256(48 * cnt + 1) + ws1 + 8192))) return rc;
+    Bump b(c->ws, c->ws_cap);
+    uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
+    void* w1 = b.take<uint8_t>(ws1);
+    if (cnt) HIPC(hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s));
+    uint8_t* part = cm->virt ? d_rows + 48 * rr : d_rows + 48 * R;
+    if ((rc = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s))) return rc;
+    // an invalid encoding anywhere: this partial becomes 48 zero bytes, itself invalid
+    LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
+    HIPC(hipStreamSynchronize(s));   // the host slice and the workspace are reused
+  }
+  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 48 * R, d_rows, 48, ncclUint8, cm->comm, s));
+  if (is_root(cm)) {   // the partials are compressed points: decode + sum them on rank 0
+    const uint32_t offR[2] = {0, (uint32_t)R};
+    const size_t wsR = agg_ws_bytes(0, 1, offR);
+    if ((rc = ensure_ws(c, wsR + 4096))) return rc;
+    if ((rc = agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s))) return rc;
+  }
+  if (!cm->virt) {
+    NCCLC(api, api->broadcast(d_sum, d_sum, 48, ncclUint8, 0, cm->comm, s));
+    NCCLC(api, api->broadcast(d_st + 1, d_st + 1, 4, ncclUint8, 0, cm->comm, s));
+  }
+  int32_t st = 0;
+  HIPC(hipMemcpyAsync(out, d_sum, 48, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(&st, d_st + 1, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  return st;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
+                                         const uint8_t* msgs, size_t msg_len, const uint8_t* sigs,
+                                         const uint8_t* dom8s, uint8_t* verdicts) try {
+  if (!call_off || !sigs || !dom8s || !verdicts || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
+  if (call_off[n_calls] && (!pks || (!msgs && msg_len))) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  Comm* cm = comm_ctx(&rc);
+  if (!cm) return rc;
+  RcclApi* api = cm->virt ? nullptr : rccl_api();
+  if (!cm->virt && !api) return BLS381_ENODEV;
+  const size_t R = (size_t)cm->nranks;
+  const size_t base = n_calls / R, extra = n_calls % R, width = base + (extra ? 1 : 0);
+  if (width == 0) return 0;
+  std::vector<uint8_t> rows(width * R, 0);
+  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
+    const size_t rr = (size_t)r;
+    const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
+    if (!cnt) continue;
+    std::vector<uint32_t> off(cnt + 1);
+    for (size_t k = 0; k <= cnt; ++k) off[k] = call_off[lo + k] - call_off[lo];
+    const size_t k0 = call_off[lo];
+    if ((rc = bls381_verify_multiple_batch(cnt, off.data(), pks ? pks + 48 * k0 : nullptr,
+                                           msgs ? msgs + msg_len * k0 : nullptr, msg_len, sigs + 96 * lo,
+                                           dom8s + 8 * lo, rows.data() + width * rr)))
+      return rc;
+  }
+  if (!cm->virt) {   // all-gather the verdict rows (each rank filled its own)
+    std::lock_guard<std::mutex> lk(c->mu);
+    hipStream_t s = c->stream;
+    uint8_t* d_rows;
+    if ((rc = comm_rows(cm, width * (R + 1), &d_rows))) return rc;
+    HIPC(hipMemcpyAsync(d_rows + width * R, rows.data() + width * (size_t)cm->rank, width, hipMemcpyHostToDevice, s));
+    NCCLC(api, api->all_gather(d_rows + width * R, d_rows, width, ncclUint8, cm->comm, s));
+    HIPC(hipMemcpyAsync(rows.data(), d_rows, width * R, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+  }
+  for (size_t q = 0; q < R; ++q) {
+    const size_t qlo = q * base + (q < extra ? q : extra), qcnt = base + (q < extra ? 1 : 0);
+    std::memcpy(verdicts + qlo, rows.data() + width * q, qcnt);
+  }
   return 0;
 } catch (const std::exception& e) {
   t_err = e.what();

@@ -167,6 +167,38 @@ int bls381_miller_partial(size_t n, const uint8_t* pks, const uint8_t* msgs, siz
 /* Multiply k partial products and run one final exponentiation: 1 / 0. */
 int bls381_final_verify(size_t k, const uint8_t* parts576);
 
+/* ---- native multi-GPU over RCCL: one process per GPU -------- */
+/* A communicator lives inside the library (RCCL opened with dlopen on first
+ * use).  Rank 0 makes a 128-byte id, the launcher hands it to every rank (any
+ * channel: bls381_amd/comm.py uses TCP), each rank calls bls381_comm_init on the
+ * device it selected with bls381_init.  No PyTorch anywhere. */
+int bls381_comm_unique_id(uint8_t out[128]);
+int bls381_comm_init(int nranks, int rank, const uint8_t uid[128]);
+/* One process plays all nranks ranks on its own GPU: the same partition and
+ * rank-0 combination, the all-gather a device copy (RCCL refuses two ranks on
+ * one GPU; this is how a one-GPU box runs the N-rank protocol). */
+int bls381_comm_init_virtual(int nranks);
+int bls381_comm_size(void);   /* 0 without a communicator */
+int bls381_comm_rank(void);   /* -1 without a communicator */
+void bls381_comm_destroy(void);
+/* Collective bls_verify_multiple (every rank passes the same call): distinct
+ * message k goes to rank k mod nranks (its pubkey group never straddles ranks),
+ * rank 0 adds (sig, -g1); each rank's Miller product (576 B, zero if a member is
+ * invalid) is all-gathered over RCCL and rank 0 multiplies them and runs the one
+ * final exponentiation of the call (py_ecc's single-FE semantics,
+ * 1_custody-game.md:409); the verdict is broadcast.  Returns 1 / 0 on every rank. */
+int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len,
+                                   const uint8_t sig[96], const uint8_t dom8[8]);
+/* Collective bls_aggregate_pubkeys: contiguous pubkey ranges per rank, compressed
+ * partials all-gathered and summed on rank 0, broadcast.  Returns 0 or
+ * BLS381_EINVAL_POINT (any rank's invalid encoding) on every rank. */
+int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]);
+/* Independent verify_multiple calls, contiguous call ranges per rank (a call's
+ * final exponentiation is never split); every rank receives all verdicts. */
+int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
+                                         const uint8_t* msgs, size_t msg_len, const uint8_t* sigs,
+                                         const uint8_t* dom8s, uint8_t* verdicts);
+
 /* ---- device-resident pubkey registry ---------------- */
 /* Decoded validator pubkeys kept in HBM, so committee aggregation reads each
  * member's point instead of decompressing it (the per-key Fp square root that

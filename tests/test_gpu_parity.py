@@ -737,3 +737,57 @@ def test_verify_multiple_batch_device_entry(native, golden, torsion):
     del off, msgs                                   # the plan is the engine's own copy
     got = d_v.cpu().tolist()
     assert got == [int(e) for _, e in cases]
+
+
+# ------------------------------------ native multi-GPU ABI over RCCL
+def _comm_checks(native, golden, torsion):
+    from bls381_amd import comm
+    _, gb = golden
+    h = bytes.fromhex
+    native.set_subgroup_policy("pyecc")
+    vms = [(c, c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+    vms += [(c, c["expected_pyecc"]) for c in torsion["verify_multiple"]]
+    for c, want in vms:
+        got = comm.verify_multiple([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]),
+                                   int(c["domain"]))
+        assert got == want, c["kind"]
+    for c in gb["aggregate_pubkeys"] + torsion["aggregate_pubkeys"]:
+        assert comm.aggregate_pubkeys([h(p) for p in c["input"]]).hex() == c["output"], c["kind"]
+    keys = [O.privtopub(k) for k in range(1, 41)]
+    assert comm.aggregate_pubkeys([keys[i % 40] for i in range(1000)]) == O.privtopub(
+        sum((i % 40) + 1 for i in range(1000)))
+    with pytest.raises(ValueError):
+        comm.aggregate_pubkeys(keys[:7] + [h(gb["invalid_g1"][1])])
+    off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+    for c, _ in vms * 2:
+        pks += b"".join(h(p) for p in c["pubkeys"]); msgs += b"".join(h(m) for m in c["messages"])
+        sigs += h(c["signature"]); doms += int(c["domain"]).to_bytes(8, "big")
+        off.append(off[-1] + len(c["pubkeys"]))
+    assert comm.verify_multiple_batch(off, pks, msgs, 32, sigs, doms) == [w for _, w in vms * 2]
+
+
+def test_native_comm_rccl_world1(native, golden, torsion):
+    """The library's own RCCL communicator (ncclCommInitRank through dlopen), one rank: the
+    collective entry points give the single-GPU verdicts and bytes.  Multi-rank RCCL on a
+    one-GPU box is refused by RCCL itself (duplicate GPU), see the virtual-rank test."""
+    from bls381_amd import comm
+    comm.init(1, 0, comm.unique_id())
+    try:
+        assert comm.size() == 1 and comm.rank() == 0
+        _comm_checks(native, golden, torsion)
+    finally:
+        comm.destroy()
+    assert comm.size() == 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_native_comm_virtual_ranks(native, golden, torsion, world):
+    """N ranks on one GPU (bls381_comm_init_virtual): per-rank partials by distinct message,
+    rank-0 product + single final exponentiation, contiguous aggregation ranges -- no PyTorch."""
+    from bls381_amd import comm
+    comm.init_virtual(world)
+    try:
+        assert comm.size() == world
+        _comm_checks(native, golden, torsion)
+    finally:
+        comm.destroy()
