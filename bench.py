@@ -82,6 +82,7 @@ def make_workload(native, n, seed):
     pks = native.privtopub_batch(sks)
     sigs = bytearray(native.sign_batch(bytes(msgs), sks, doms))
     sk_ints = [int.from_bytes(sks[32 * i:32 * i + 32], "big") for i in range(n)]
+    make_workload.clean = (bytes(msgs), bytes(sigs))     # before tampering (randomized-batch line)
     expected = np.ones(n, dtype=bool)
     for i in range(3, n, 16):              # 1/16 tampered, full verification work
         if (i // 16) % 2 == 0:
@@ -538,6 +539,43 @@ def bench_native_comm(native, args, world, rank, dist, dev):
     return out
 
 
+def bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, dist, dev, stream, t_u8):
+    """Opt-in randomized batch verification (bls381_verify_batch_randomized_device): sub-batches
+    of 64 items share one final exponentiation; per-item verdicts (failing sub-batches are
+    re-verified item by item).  On the clean C2 batch, and on the bench's 1/16-tampered one
+    (nearly every sub-batch then fails: the fallback cost)."""
+    import torch
+    n = len(pks) // 48
+    B = 64
+    clean_msgs, clean_sigs = make_workload.clean
+    out = {"sub_batch": B}
+    ws = torch.empty(L.bls381_verify_batch_randomized_workspace_size(n, B), dtype=torch.uint8, device=dev)
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    for name, m, sg, want in (("clean", clean_msgs, clean_sigs, np.ones(n, dtype=bool)),
+                              ("tampered_1_in_16", msgs, sigs, expected)):
+        d = [t_u8(pks), t_u8(m), t_u8(sg), t_u8(doms)]
+        st = (ctypes.c_uint64 * 3)()
+
+        def step():
+            native.check(L.bls381_verify_batch_randomized_device(
+                n, *[x.data_ptr() for x in d], os.urandom(32), B, d_v.data_ptr(), ws.data_ptr(),
+                ctypes.c_void_p(stream.cuda_stream), st))
+        step()
+        assert np.array_equal(d_v.cpu().numpy().astype(bool), want), "randomized verdict mismatch (%s)" % name
+        steps = max(args.steps, 3)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        t = _max_time(time.perf_counter() - t0, world, dist, dev)
+        out[name] = {"verifications_per_s": n * steps * world / t, "ms_per_step": 1e3 * t / steps,
+                     "accepted_in_batches": int(st[0]), "verified_singly": int(st[1]), "failed_sub_batches": int(st[2])}
+    return out
+
+
 def bench_latency(native, pks, msgs, sigs, expected):
     """Single-call latency through the drop-in shim (the reference calls BLS one signature at a
     time: 0_beacon-chain.md:1594,1603,1664,1756,1796,1824): bls_verify and an attestation-shaped
@@ -693,6 +731,8 @@ def main():
     sec = {}
     if not args.no_secondary:
         sec["c2_deposits"] = bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8)
+        sec["c2_randomized_batch"] = bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, dist,
+                                                      dev, stream, t_u8)
         sec["c3_epoch"] = bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist)
         sec["c4_aggregate"] = bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist)
         sec["c5_multi_pairing"] = bench_c5(native, args, world, rank, dist, dev)

@@ -46,6 +46,11 @@ _SIGS = {
     "bls381_verify_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p]),
     "bls381_verify_batch_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t]),
     "bls381_verify_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p]),
+    "bls381_verify_batch_randomized": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p, ctypes.c_size_t,
+                                                      _u8p]),
+    "bls381_verify_batch_randomized_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t, ctypes.c_size_t]),
+    "bls381_verify_batch_randomized_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p,
+                                                             ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p]),
     "bls381_aggregate_pubkeys_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p]),
     "bls381_aggregate_pubkeys_batch_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t, ctypes.c_size_t]),
     "bls381_aggregate_pubkeys_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, _u8p,
@@ -240,6 +245,17 @@ def verify_batch(pks: bytes, msgs32: bytes, sigs: bytes, dom8s: bytes) -> np.nda
     if n:
         check(lib().bls381_verify_batch(n, _buf(pks), _buf(msgs32), _buf(sigs), _buf(dom8s),
                                         out.ctypes.data_as(ctypes.c_void_p)))
+    return out.astype(bool)
+
+
+def verify_batch_randomized(pks: bytes, msgs32: bytes, sigs: bytes, dom8s: bytes, seed: bytes,
+                            batch: int = 64) -> np.ndarray:
+    """Opt-in randomized batch verification (bls381_verify_batch_randomized); per-item verdicts."""
+    n = len(pks) // 48
+    out = np.zeros(n, dtype=np.uint8)
+    if n:
+        check(lib().bls381_verify_batch_randomized(n, _buf(pks), _buf(msgs32), _buf(sigs), _buf(dom8s), _buf(seed),
+                                                   batch, out.ctypes.data_as(ctypes.c_void_p)))
     return out.astype(bool)
 
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -306,15 +307,18 @@ size_t agg_ws_size(const AggPlan& p, int ncomp) {
   return s;
 }
 
-// runs the plan; returns device pointers to the final per-group Jacobian sums / bad flags
+// runs the plan; returns device pointers to the final per-group Jacobian sums / bad flags.
+// Level 0 decodes compressed points (d_in), reads registry entries (reg), or -- with
+// jac_in -- sums Jacobian SoA points (n_jac_in of them, bad flags bad_in).
 template <class F>
 int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStream_t s,
             const uint32_t** out_jac, const uint8_t** out_bad, size_t* used, size_t cap = SIZE_MAX,
-            const agg_reg_src* reg = nullptr, int check = 0) {
+            const agg_reg_src* reg = nullptr, int check = 0, const uint32_t* jac_in = nullptr,
+            const uint8_t* bad_in = nullptr, size_t n_jac_in = 0) {
   Bump b(ws, cap);
-  const uint32_t* prev_jac = nullptr;
-  const uint8_t* prev_bad = nullptr;
-  size_t prev_n = 0;
+  const uint32_t* prev_jac = jac_in;
+  const uint8_t* prev_bad = bad_in;
+  size_t prev_n = n_jac_in;
   for (size_t l = 0; l < p.levels.size(); ++l) {
     const auto& lv = p.levels[l];
     agg_chunk* d_chunks = b.take<agg_chunk>(lv.size());
@@ -324,21 +328,21 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
     const agg_reg_src none{nullptr, nullptr, nullptr, 0, 0};
     size_t n_in_total = 0;
     for (const auto& ch : lv) n_in_total += ch.end - ch.begin;
-    const bool lanes = std::is_same<F, fp_t>::value && l == 0 && n_in_total < AGG_LANE_AVG_MAX * lv.size();
-    if (lanes) {
+    const bool lanes = std::is_same<F, fp_t>::value && l == 0 && !jac_in && n_in_total < AGG_LANE_AVG_MAX * lv.size();
+    if (l > 0 || jac_in) {
+      LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_JAC>), (size_t)lv.size(),
+             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad, none, 0);
+    } else if (lanes) {
       LAUNCH("agg_lane_sum", s, dim3(grid_for(lv.size())), dim3(KBLOCK), k_agg_lanes<AGG_REGISTRY>, (size_t)lv.size(),
              (const agg_chunk*)d_chunks, d_in, jac, bad, reg ? *reg : none, check);
     } else if (l == 0 && reg) {
       LAUNCH("agg_registry_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_REGISTRY>),
              (size_t)lv.size(), (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0,
              (const uint8_t*)nullptr, jac, bad, *reg, check);
-    } else if (l == 0) {
+    } else {
       LAUNCH("agg_decode_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_BYTES>), (size_t)lv.size(),
              (const agg_chunk*)d_chunks, d_in, (const uint32_t*)nullptr, (size_t)0, (const uint8_t*)nullptr, jac, bad,
              none, check);
-    } else {
-      LAUNCH("agg_sum", s, dim3((unsigned)lv.size()), dim3(KBLOCK), (k_agg_chunks<F, AGG_JAC>), (size_t)lv.size(),
-             (const agg_chunk*)d_chunks, (const uint8_t*)nullptr, prev_jac, prev_n, prev_bad, jac, bad, none, 0);
     }
     prev_jac = jac;
     prev_bad = bad;
@@ -1925,6 +1929,200 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
     const size_t qlo = q * base + (q < extra ? q : extra), qcnt = base + (q < extra ? 1 : 0);
     std::memcpy(verdicts + qlo, rows.data() + width * q, qcnt);
   }
+  return 0;
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+}  // extern "C"
+
+// ------------------------------------------ randomized batch verification --
+// Opt-in small-exponent batch test over independent bls_verify items (kernels:
+// bls381_kernels.hpp "randomized batch verification").  Per-item verdicts are
+// kept: a sub-batch that fails, and every item whose signature is outside G2, is
+// re-verified item by item with the default pipeline.
+namespace {
+
+size_t rb_ws_size(size_t n, size_t B) {
+  const size_t nb = (n + B - 1) / B, nslots = nb * (B / 2 + 1);
+  size_t s = verify_ws_size(n) + 4 * 65536;
+  s += align256(2 * FPW * n) + 3 * align256(n) + align256(6 * FPW * n) + align256(n);   // R1, statuses, R2, zeros
+  const size_t ch = nb + n / CHUNK_L1 + 1;                                              // R2 sums per sub-batch
+  s += 3 * (align256(ch * sizeof(agg_chunk)) + align256(ch * 6 * FPW) + align256(ch));
+  s += align256(4 * FPW * nb) + align256(nb);                                           // signature sums
+  s += 2 * (align256(12 * FPW * nslots) + align256(nslots) + align256(nslots * sizeof(agg_chunk)));
+  s += 2 * align256(nb) + align256(64);
+  s += align256(184 * n) + align256(4 * n) + align256(n) + verify_ws_size(n);           // the per-item fallback
+  return s;
+}
+
+int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
+                          const uint8_t* doms, const uint8_t* seed32, size_t B, uint8_t* d_verdicts, void* ws,
+                          size_t ws_cap, hipStream_t s, uint64_t* stats) {
+  const size_t nb = (n + B - 1) / B, half = B / 2, nslots = nb * (half + 1);
+  Bump b(ws, ws_cap);
+  VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n)), n);
+  uint32_t* r1 = b.take<uint32_t>(2 * FP_LIMBS * n);
+  uint8_t* r1_st = b.take<uint8_t>(n);
+  uint8_t* cls = b.take<uint8_t>(n);
+  uint32_t* r2 = b.take<uint32_t>(6 * FP_LIMBS * n);
+  uint8_t* zeros = b.take<uint8_t>(n);
+  uint8_t* d_seed = b.take<uint8_t>(64);
+  const dim3 g1(grid_for(n)), g2(grid_for(2 * n)), blk(KBLOCK);
+  const int chk = check_subgroups();
+  auto seed = std::make_shared<std::vector<uint8_t>>(seed32, seed32 + 32);
+  HIPC(hipMemcpyAsync(d_seed, seed->data(), 32, hipMemcpyHostToDevice, s));
+  HIPC(hipMemsetAsync(zeros, 0, n, s));
+  {
+    std::lock_guard<std::mutex> lk(c->fork_mu);
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    LAUNCH("decode_g1", c->side, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
+    LAUNCH("decode_g2", c->side, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
+    HIPC(hipEventRecord(c->ev_join, c->side));
+    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st);
+    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+  }
+  LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
+         (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
+  LAUNCH("rb_scale_g2", s, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
+         (const uint8_t*)w.sig_st, (const uint8_t*)cls, r2);
+  // per sub-batch sum of [r_i] sig_i
+  std::vector<uint32_t> off(nb + 1);
+  for (size_t k = 0; k <= nb; ++k) off[k] = (uint32_t)std::min(n, k * B);
+  auto plan = std::make_shared<AggPlan>(plan_agg(nb, off.data()));
+  const uint32_t* sjac;
+  const uint8_t* sbad;
+  size_t used = 0;
+  uint8_t* sub = b.take<uint8_t>(0);
+  int rc = run_agg<fp2p_t>(*plan, nb, nullptr, sub, s, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n);
+  if (rc) return rc;
+  b.off += used;
+  uint32_t* s_aff = b.take<uint32_t>(4 * FP_LIMBS * nb);
+  uint8_t* s_st = b.take<uint8_t>(nb);
+  LAUNCH("agg_g2_affine", s, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
+  // Miller values: B/2 two-pair slots per sub-batch + its signature-sum slot
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nslots);
+  uint8_t* fst = b.take<uint8_t>(nslots);
+  const size_t nitems = nb * half;
+  LAUNCH("rb_miller_items", s, dim3(grid_for(2 * nitems)), blk, k_rb_miller_items, n, half, nitems,
+         (const uint32_t*)w.h_aff, (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st,
+         (const uint8_t*)cls, nslots, f, fst);
+  LAUNCH("rb_miller_sig", s, dim3(grid_for(2 * nb)), blk, k_rb_miller_sig, nb, half, (const uint32_t*)s_aff,
+         (const uint8_t*)s_st, nslots, f, fst);
+  std::vector<uint32_t> seg(nb + 1);
+  for (size_t k = 0; k <= nb; ++k) seg[k] = (uint32_t)(k * (half + 1));
+  auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products(seg));
+  size_t n_in = nslots;
+  for (const auto& chunks : *passes) {
+    agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
+    uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
+    uint8_t* nst = b.take<uint8_t>(chunks.size());
+    HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+    LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), blk, k_fp12_chunk_product, chunks.size(),
+           (const agg_chunk*)d_ch, (const uint32_t*)f, n_in, (const uint8_t*)fst, nf, nst);
+    f = nf;
+    fst = nst;
+    n_in = chunks.size();
+  }
+  uint8_t* bv = b.take<uint8_t>(nb);
+  LAUNCH("final_exp", s, dim3(grid_for(2 * nb)), blk, k_final_exp_verdict, nb, (const uint32_t*)f,
+         (const uint8_t*)fst, bv);
+  std::vector<uint8_t> h_bv(nb), h_cls(n);
+  HIPC(hipMemcpyAsync(h_bv.data(), bv, nb, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(h_cls.data(), cls, n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));   // the plans and the seed copy are done with as well
+  // verdicts: bad -> 0; batched in a passing sub-batch -> 1; the rest one by one
+  std::vector<uint8_t> v(n, 0);
+  std::vector<uint32_t> single;
+  uint64_t n_batched = 0, n_failed = 0;
+  for (size_t k = 0; k < nb; ++k) n_failed += h_bv[k] ? 0 : 1;
+  for (size_t i = 0; i < n; ++i) {
+    if (h_cls[i] == RB_BAD) continue;
+    if (h_cls[i] == RB_BATCH && h_bv[i / B]) { v[i] = 1; ++n_batched; continue; }
+    single.push_back((uint32_t)i);
+  }
+  if (stats) { stats[0] = n_batched; stats[1] = single.size(); stats[2] = n_failed; }
+  const size_t m = single.size();
+  if (m) {
+    uint32_t* d_idx = b.take<uint32_t>(m);
+    uint8_t* gp = b.take<uint8_t>(48 * m);
+    uint8_t* gm = b.take<uint8_t>(32 * m);
+    uint8_t* gs = b.take<uint8_t>(96 * m);
+    uint8_t* gd = b.take<uint8_t>(8 * m);
+    uint8_t* gv = b.take<uint8_t>(m);
+    void* vws = b.take<uint8_t>(verify_ws_size(m));
+    HIPC(hipMemcpyAsync(d_idx, single.data(), 4 * m, hipMemcpyHostToDevice, s));
+    LAUNCH("gather_rows", s, dim3(grid_for(48 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, pks, 48u, gp);
+    LAUNCH("gather_rows", s, dim3(grid_for(32 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, msgs, 32u, gm);
+    LAUNCH("gather_rows", s, dim3(grid_for(96 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, sigs, 96u, gs);
+    LAUNCH("gather_rows", s, dim3(grid_for(8 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, doms, 8u, gd);
+    if ((rc = run_verify_batch(c, m, gp, gm, gs, gd, gv, vws, s))) return rc;
+    std::vector<uint8_t> h_gv(m);
+    HIPC(hipMemcpyAsync(h_gv.data(), gv, m, hipMemcpyDeviceToHost, s));
+    HIPC(hipStreamSynchronize(s));
+    for (size_t k = 0; k < m; ++k) v[single[k]] = h_gv[k];
+  }
+  HIPC(hipMemcpyAsync(d_verdicts, v.data(), n, hipMemcpyHostToDevice, s));
+  HIPC(hipStreamSynchronize(s));
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t bls381_verify_batch_randomized_workspace_size(size_t n, size_t batch) {
+  return (batch < 2 || batch % 2) ? 0 : rb_ws_size(n ? n : 1, batch);
+}
+
+int bls381_verify_batch_randomized_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32,
+                                          const uint8_t* d_sigs, const uint8_t* d_dom8s, const uint8_t seed[32],
+                                          size_t batch, uint8_t* d_verdicts, void* d_workspace, void* stream,
+                                          uint64_t* stats) try {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n == 0) return 0;
+  if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !seed || !d_verdicts || !d_workspace || batch < 2 || batch % 2)
+    return BLS381_EARG;
+  return run_verify_randomized(c, n, d_pks, d_msgs32, d_sigs, d_dom8s, seed, batch, d_verdicts, d_workspace,
+                               rb_ws_size(n, batch), (hipStream_t)stream, stats);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+int bls381_verify_batch_randomized(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
+                                   const uint8_t* dom8s, const uint8_t seed[32], size_t batch,
+                                   uint8_t* verdicts_out) try {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n == 0) return 0;
+  if (!pks || !msgs32 || !sigs || !dom8s || !seed || !verdicts_out || batch < 2 || batch % 2) return BLS381_EARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  const size_t in_bytes = align256(48 * n) + align256(32 * n) + align256(96 * n) + align256(8 * n) + align256(n);
+  const size_t wsb = rb_ws_size(n, batch);
+  if ((rc = ensure_ws(c, in_bytes + wsb + 1024))) return rc;
+  Bump b(c->ws, c->ws_cap);
+  uint8_t* d_pks = b.take<uint8_t>(48 * n);
+  uint8_t* d_msgs = b.take<uint8_t>(32 * n);
+  uint8_t* d_sigs = b.take<uint8_t>(96 * n);
+  uint8_t* d_doms = b.take<uint8_t>(8 * n);
+  uint8_t* d_v = b.take<uint8_t>(n);
+  void* ws = b.take<uint8_t>(wsb);
+  hipStream_t s = c->stream;
+  HIPC(hipMemcpyAsync(d_pks, pks, 48 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_msgs, msgs32, 32 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_sigs, sigs, 96 * n, hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_doms, dom8s, 8 * n, hipMemcpyHostToDevice, s));
+  if ((rc = run_verify_randomized(c, n, d_pks, d_msgs, d_sigs, d_doms, seed, batch, d_v, ws, wsb, s, nullptr)))
+    return rc;
+  HIPC(hipMemcpyAsync(verdicts_out, d_v, n, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
   return 0;
 } catch (const std::exception& e) {
   t_err = e.what();

@@ -13,7 +13,8 @@
 
 namespace bls381 {
 
-enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2 };
+// ST_NOSUB: decodes, but is not in G2 (randomized batching routes it to the per-item path)
+enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2, ST_NOSUB = 3 };
 
 // Subgroup policy (include/bls381.h BLS381_POLICY_*; DESIGN.md "Subgroup policy").
 //   PYECC:  py_ecc 1.7.0's checks only -- on-curve decoding, no subgroup test; the
@@ -129,7 +130,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n
   if (s == PT_OK) soa_st_g1(out, n, i, a);
 }
 
-// signatures -> affine G2 (pair SoA, 2 Fp2) + status; optional subgroup check
+// signatures -> affine G2 (pair SoA, 2 Fp2) + status; check_subgroup: 0 none,
+// 1 a point outside G2 is ST_BAD, 2 it is ST_NOSUB (and its point is stored)
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n, const uint8_t* __restrict__ sigs,
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      int check_subgroup) {
@@ -137,9 +139,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n
   if (i >= n) return;
   aff_t<fp2p_t> a;
   int s = g2_decompress(a, sigs + 96 * i);
-  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = PT_BAD;
+  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = check_subgroup == 2 ? ST_NOSUB : PT_BAD;
   if (!pr_odd()) st[i] = (uint8_t)s;
-  if (s == PT_OK) soa_st_g2(out, n, i, a);
+  if (s == PT_OK || s == ST_NOSUB) soa_st_g2(out, n, i, a);
 }
 
 // (msg, dom8) -> hash_to_G2 affine (pair SoA).  dom_stride 0 = one shared domain.
@@ -252,6 +254,130 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   const fp12p_t f = soa_ld12(f_in, n, i);
   const bool one = fp12_is_one(final_exp(f));
   if (lead) verdict[i] = one ? 1 : 0;
+}
+
+// ------------------------------------- randomized batch verification (opt-in) --
+// Small-exponent batch test (SURVEY.md §7 "Verdict semantics under batching"):
+// a sub-batch of items verifies when
+//   prod_i e(H(m_i), [r_i] pk_i) * e(sum_i [r_i] sig_i, -g1) == 1
+// with independent 64-bit r_i; one final exponentiation per sub-batch.  Only
+// items whose signature lies in G2 enter a sub-batch (the pairing is linear in
+// that argument only on G2); the others, and every item of a failing sub-batch,
+// are verified one by one.
+enum : uint8_t { RB_BAD = 0, RB_BATCH = 1, RB_SINGLE = 2 };
+
+// r_i = the first 8 bytes of SHA-256(seed || i), i as 8 little-endian bytes; never 0
+__device__ __forceinline__ uint64_t rb_scalar(const uint8_t* seed32, uint64_t i) {
+  uint8_t buf[40];
+  for (int k = 0; k < 32; ++k) buf[k] = seed32[k];
+  for (int k = 0; k < 8; ++k) buf[32 + k] = (uint8_t)(i >> (8 * k));
+  uint32_t d[8];
+  sha256(d, buf, 40);
+  const uint64_t r = ((uint64_t)d[0] << 32) | d[1];
+  return r ? r : 1;
+}
+
+// per item, one lane: its class, and R1 = [r_i] pk_i affine (status OK / INF)
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t n, const uint8_t* __restrict__ seed32,
+                                                       const uint32_t* __restrict__ pk_aff,
+                                                       const uint8_t* __restrict__ pk_st,
+                                                       const uint8_t* __restrict__ sig_st,
+                                                       uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
+                                                       uint8_t* __restrict__ cls) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  const uint8_t ps = pk_st[i], ss = sig_st[i];
+  const uint8_t c = (ps == ST_BAD || ss == ST_BAD) ? RB_BAD : (ss == ST_NOSUB ? RB_SINGLE : RB_BATCH);
+  cls[i] = c;
+  uint8_t st = ST_INF;
+  if (c == RB_BATCH && ps == ST_OK) {
+    aff_t<fp_t> a;
+    if (jac_to_aff(a, jac_mul_u64(soa_ld_g1(pk_aff, n, i), rb_scalar(seed32, i)))) {
+      soa_st_g1(r1_aff, n, i, a);
+      st = ST_OK;
+    }
+  }
+  r1_st[i] = st;
+}
+
+// per item, one lane pair: R2 = [r_i] sig_i (Jacobian SoA; infinity when the item is not batched)
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g2(size_t n, const uint8_t* __restrict__ seed32,
+                                                       const uint32_t* __restrict__ sig_aff,
+                                                       const uint8_t* __restrict__ sig_st,
+                                                       const uint8_t* __restrict__ cls,
+                                                       uint32_t* __restrict__ r2_jac) {
+  const size_t i = item_index<2>();
+  if (i >= n) return;
+  jac_t<fp2p_t> r = jac_infinity<fp2p_t>();
+  if (cls[i] == RB_BATCH && sig_st[i] == ST_OK) r = jac_mul_u64(soa_ld_g2(sig_aff, n, i), rb_scalar(seed32, i));
+  soa_jac<fp2p_t>::st(r2_jac, n, i, r);
+}
+
+// per sub-batch: sum of the R2 -> affine + status
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g2_affine(size_t ng, const uint32_t* __restrict__ jac,
+                                                         const uint8_t* __restrict__ bad,
+                                                         uint32_t* __restrict__ out_aff, uint8_t* __restrict__ st) {
+  const size_t g = item_index<2>();
+  if (g >= ng) return;
+  const bool lead = !pr_odd();
+  if (bad[g]) { if (lead) st[g] = ST_BAD; return; }
+  aff_t<fp2p_t> a;
+  if (!jac_to_aff(a, soa_jac<fp2p_t>::ld(jac, ng, g))) { if (lead) st[g] = ST_INF; return; }
+  soa_st_g2(out_aff, ng, g, a);
+  if (lead) st[g] = ST_OK;
+}
+
+// Miller values of one sub-batch layout: sub-batch b owns slots [b (B/2 + 1), (b + 1)(B/2 + 1)):
+// B/2 item slots (lane pair j: items 2j, 2j + 1, pairs (H, R1)) and the signature-sum slot.
+// Item slots past the last item hold 1.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_items(size_t n, size_t half_b, size_t nslots_items,
+                                                           const uint32_t* __restrict__ h_aff,
+                                                           const uint8_t* __restrict__ h_st,
+                                                           const uint32_t* __restrict__ r1_aff,
+                                                           const uint8_t* __restrict__ r1_st,
+                                                           const uint8_t* __restrict__ cls, size_t nslots,
+                                                           uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t j = item_index<2>();
+  if (j >= nslots_items) return;
+  const size_t slot = (j / half_b) * (half_b + 1) + j % half_b;
+  aff_t<fp2p_t> Q[2];
+  g1_line_pre P[2];
+  int np = 0;
+  for (int t = 0; t < 2; ++t) {
+    const size_t i = 2 * j + t;
+    if (i < n && cls[i] == RB_BATCH && r1_st[i] == ST_OK && h_st[i] == ST_OK) {
+      Q[np] = soa_ld_g2(h_aff, n, i);
+      P[np] = g1_prepare(soa_ld_g1(r1_aff, n, i));
+      ++np;
+    }
+  }
+  fp12p_t f;
+  bool degen = false;
+  if (np == 2) f = miller_loop_n<2>(Q, P, degen);
+  else if (np == 1) f = miller_loop_n<1>(Q, P, degen);
+  else f = fp12_one<fp2p_t>();
+  soa_st12(f_out, nslots, slot, f);
+  if (!pr_odd()) st_out[slot] = degen ? ST_BAD : ST_OK;
+}
+
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t half_b,
+                                                         const uint32_t* __restrict__ s_aff,
+                                                         const uint8_t* __restrict__ s_st, size_t nslots,
+                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t b = item_index<2>();
+  if (b >= nb) return;
+  const size_t slot = b * (half_b + 1) + half_b;
+  fp12p_t f = fp12_one<fp2p_t>();
+  bool degen = false;
+  const uint8_t st = s_st[b];
+  if (st == ST_OK) {
+    aff_t<fp2p_t> Q = soa_ld_g2(s_aff, nb, b);
+    aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+    g1_line_pre P = g1_prepare(ng);
+    f = miller_loop_n<1>(&Q, &P, degen);
+  }
+  soa_st12(f_out, nslots, slot, f);
+  if (!pr_odd()) st_out[slot] = (st == ST_BAD || degen) ? ST_BAD : ST_OK;
 }
 
 // ---------------------------------------------------- aggregation kernels --

@@ -124,6 +124,28 @@ int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_
                                const uint8_t* d_sigs, const uint8_t* d_dom8s, uint8_t* d_verdicts,
                                void* d_workspace, void* stream);
 
+/* Opt-in randomized batch verification of n independent bls_verify items (the
+ * north star's "batched Miller loops share a single final exponentiation"; SURVEY
+ * §7 "Verdict semantics under batching").  Items go in sub-batches of `batch`
+ * (even, >= 2); a sub-batch passes when
+ *     prod_i e(H(m_i), [r_i] pk_i) * e(sum_i [r_i] sig_i, -g1) == 1,
+ * r_i = first 8 bytes of SHA-256(seed || i) (seed: 32 caller-chosen random bytes),
+ * with one final exponentiation.  Items of a passing sub-batch are valid (a wrong
+ * one slips through with probability <= 2^-63); every item of a failing sub-batch,
+ * and every item whose signature is outside G2, is re-verified alone by the
+ * default pipeline, so verdicts are the per-item ones.  The device form takes
+ * device buffers, runs synchronously (the re-verification needs the sub-batch
+ * results on the host) and, when stats != NULL, stores [items accepted in passing
+ * sub-batches, items verified one by one, failed sub-batches]. */
+int bls381_verify_batch_randomized(size_t n, const uint8_t* pks, const uint8_t* msgs32, const uint8_t* sigs,
+                                   const uint8_t* dom8s, const uint8_t seed[32], size_t batch,
+                                   uint8_t* verdicts_out);
+size_t bls381_verify_batch_randomized_workspace_size(size_t n, size_t batch);
+int bls381_verify_batch_randomized_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32,
+                                          const uint8_t* d_sigs, const uint8_t* d_dom8s, const uint8_t seed[32],
+                                          size_t batch, uint8_t* d_verdicts, void* d_workspace, void* stream,
+                                          uint64_t* stats);
+
 /* Committee aggregation (config C3/C4): n_groups groups, group g = pubkeys
  * [offsets[g], offsets[g+1]).  out48 receives n_groups compressed sums; status[g]
  * is 0, or BLS381_EINVAL_POINT when a member does not decode. */

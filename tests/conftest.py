@@ -27,7 +27,15 @@ def golden():
 
 @pytest.fixture(scope="session")
 def native():
-    """The HIP engine; GPU tests fail loudly if it is not loadable."""
+    """The HIP engine; GPU tests fail loudly if it is not loadable.
+
+    Some GPU tests hand torch-allocated device buffers to the engine.  The torch
+    wheel bundles its own HIP runtime: it has to be loaded before the engine's
+    (bench.py imports torch first too), so that both use one runtime."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     from bls381_amd import _native
     _native.init(0)
     return _native

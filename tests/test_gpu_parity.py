@@ -791,3 +791,75 @@ def test_native_comm_virtual_ranks(native, golden, torsion, world):
         _comm_checks(native, golden, torsion)
     finally:
         comm.destroy()
+
+
+# ------------------------- opt-in randomized batch verification (north star)
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_randomized_batch_matches_per_item_verdicts(native, golden, torsion, policy):
+    """Golden + torsion verify items (bad encodings, infinities, torsion in keys and signatures)
+    through bls381_verify_batch_randomized at several sub-batch sizes: the same verdicts as
+    the default per-item pipeline (py_ecc's, or the strict column)."""
+    import os as _os
+    _, gb = golden
+    items = [(c, c["expected"]) for c in gb["verify"]]
+    items += [(c, c["expected_" + policy]) for c in torsion["verify"]]
+    if policy == "strict":
+        items = [(c, e) for c, e in items if "expected_strict" in c] + [(c, e) for c, e in items
+                                                                        if "expected_strict" not in c]
+    pks = b"".join(bytes.fromhex(c["pubkey"]) for c, _ in items)
+    msgs = b"".join(bytes.fromhex(c["message"]) for c, _ in items)
+    sigs = b"".join(bytes.fromhex(c["signature"]) for c, _ in items)
+    doms = b"".join(int(c["domain"]).to_bytes(8, "big") for c, _ in items)
+    native.set_subgroup_policy(policy)
+    try:
+        want = list(native.verify_batch(pks, msgs, sigs, doms))
+        if policy == "pyecc":
+            assert want == [e for _, e in items]
+        for B in (2, 8, 64):
+            got = native.verify_batch_randomized(pks, msgs, sigs, doms, _os.urandom(32), B)
+            assert list(got) == want, B
+    finally:
+        native.set_subgroup_policy("pyecc")
+
+
+def test_randomized_batch_clean_and_tampered(native):
+    """4096 valid items: every sub-batch passes (no per-item re-verification); the same batch
+    with 1/16 tampered: identical verdicts to the default pipeline, failing sub-batches re-verified."""
+    import ctypes
+    import os as _os
+    import torch
+    L = native.lib()
+    n = 4096
+    rng = np.random.default_rng(17)
+    sk = 0xC0FFEE
+    pk = O.privtopub(sk)
+    ms = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(64)]
+    ss = native.sign_batch(b"".join(ms), sk.to_bytes(32, "big") * 64, (3).to_bytes(8, "big") * 64)
+    idx = rng.integers(0, 64, n)
+    msgs = b"".join(ms[i] for i in idx)
+    sigs = bytearray(b"".join(ss[96 * i:96 * i + 96] for i in idx))
+    doms = (3).to_bytes(8, "big") * n
+    dev = torch.device("cuda", 0)
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run(sig_bytes, B):
+        d = [t(pk * n), t(msgs), t(bytes(sig_bytes)), t(doms)]
+        v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        ws = torch.empty(L.bls381_verify_batch_randomized_workspace_size(n, B), dtype=torch.uint8, device=dev)
+        st = (ctypes.c_uint64 * 3)()
+        native.check(L.bls381_verify_batch_randomized_device(n, *[x.data_ptr() for x in d], _os.urandom(32), B,
+                                                             v.data_ptr(), ws.data_ptr(),
+                                                             ctypes.c_void_p(stream.cuda_stream), st))
+        return v.cpu().numpy().astype(bool), list(st)
+
+    v, st = run(sigs, 64)
+    assert v.all() and st == [n, 0, 0]
+    for i in range(5, n, 16):
+        j = (i + 1) % n
+        if idx[j] != idx[i]:
+            sigs[96 * i:96 * i + 96] = sigs[96 * j:96 * j + 96]
+    want = native.verify_batch(pk * n, msgs, bytes(sigs), doms)
+    assert not want.all()
+    v, st = run(sigs, 64)
+    assert np.array_equal(v, want) and st[2] > 0 and st[0] + st[1] == n
