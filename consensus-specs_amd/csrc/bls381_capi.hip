@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
       const size_t c = (size_t)(-src - 1);
       Q.x = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 0));
       Q.y = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 1));
-      P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M;
+      P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
     }
     f = miller_loop_quad(Q, g1_prepare(P), act_m, degen);
   } else {

@@ -182,15 +182,26 @@ BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E>& S) {
   return R;
 }
 
+// BP(P) = [c h2]P, c = 3(x^2 - 1): the verification hash.  The verify paths pair
+// BP(H0) with the pubkey and the signature with -[c]g1 (G1_VGEN_*) instead of
+// H = [h2]H0 with pk and sig with -g1: both pairing products are the original
+// one raised to c, which is coprime to r, so "== 1" is unchanged (the reduced
+// pairing is bilinear in its G2 argument for any G1-side point; tested against
+// every torsion fixture).  Skips the [e0]S - T step of g2_mul_cofactor.
 template <class E>
-BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
+BLS_NOINLINE jac_t<E> g2_mul_bp(const aff_t<E>& p) {
   aff_t<E> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
   const jac_t<E> t1 = jac_mul_u64(p, BLS_X_ABS);                  // [|x|]P = -[x]P
   jac_t<E> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
   Q0 = jac_add(Q0, g2_psi_jac(jac_add_aff(jac_neg(t1), np)));          // + psi([x - 1]P)
-  Q0 = jac_add(Q0, g2_psi_jac(g2_psi_jac(jac_dbl(jac_from_aff(p)))));  // + psi^2(2P)
+  return jac_add(Q0, g2_psi_jac(g2_psi_jac(jac_dbl(jac_from_aff(p)))));  // + psi^2(2P)
+}
+
+template <class E>
+BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
+  const jac_t<E> Q0 = g2_mul_bp(p);
   const jac_t<E> Q1 = jac_neg(g2_psi_jac(Q0));
   const jac_t<E> Q2 = jac_neg(g2_psi_jac(Q1));
   const jac_t<E> T = jac_add(jac_add(jac_dbl(Q2), Q1), jac_neg(g2_psi_jac(Q2)));   // Q1 + 2Q2 + Q3

@@ -144,7 +144,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n
   if (s == PT_OK || s == ST_NOSUB) soa_st_g2(out, n, i, a);
 }
 
-// (msg, dom8) -> hash_to_G2 affine (pair SoA).  dom_stride 0 = one shared domain.
+// (msg, dom8) -> the verification hash BP(H0) = [3(x^2-1)] hash_to_G2(msg, dom)
+// affine (pair SoA; g2_mul_bp: every verify kernel pairs it with the pubkey and
+// the signature with -[3(x^2-1)] g1, G1_VGEN_*).  dom_stride 0 = one shared domain.
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                    const uint8_t* __restrict__ doms, int dom_stride,
                                                    uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
@@ -155,7 +157,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, 
   aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   aff_t<fp2p_t> h;
-  const bool fin = jac_to_aff(h, g2_mul_cofactor(c));
+  const bool fin = jac_to_aff(h, g2_mul_bp(c));
   if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
   if (fin) soa_st_g2(out, n, i, h);
 }
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(s
   int np = 0;
   if (ss == ST_OK) {
     Q[np] = soa_ld_g2(sig_aff, n, i);
-    aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+    aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
     P[np] = g1_prepare(ng);
     ++np;
   }
@@ -231,7 +233,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_q
     if (use_pk) {
       P = soa_ld_g1(pk_aff, n, i);
     } else {
-      P.x = G1_GEN_X_M; P.y = G1_GEN_NEGY_M;
+      P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
     }
     f = miller_loop_quad(Q, g1_prepare(P), active, degen);
   } else {
@@ -372,7 +374,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(s
   const uint8_t st = s_st[b];
   if (st == ST_OK) {
     aff_t<fp2p_t> Q = soa_ld_g2(s_aff, nb, b);
-    aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+    aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
     g1_line_pre P = g1_prepare(ng);
     f = miller_loop_n<1>(&Q, &P, degen);
   }

@@ -124,7 +124,16 @@ __device__ __forceinline__ fp2p_t fp2_neg(const fp2p_t& a) { return pr_make(fp_n
 __device__ __forceinline__ fp2p_t fp2_dbl(const fp2p_t& a) { return pr_make(fp_dbl(a.v)); }
 __device__ __forceinline__ fp2p_t fp2_half(const fp2p_t& a) { return pr_make(fp_half(a.v)); }
 __device__ __forceinline__ fp2p_t fp2_add_lazy(const fp2p_t& a, const fp2p_t& b) { return pr_make(fp_add_lazy(a.v, b.v)); }
+#if BLS_FP2_INLINE == 2
+__device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) {
+  BLS_PHASE();
+  const fp_t r = fp_mul_body(a.v, s);
+  BLS_PHASE();
+  return pr_make(r);
+}
+#else
 __device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) { return pr_make(fp_mul(a.v, s)); }
+#endif
 __device__ __forceinline__ fp2p_t fp2_mul_small(const fp2p_t& a, int k) { return pr_make(fp_mul_small(a.v, k)); }
 __device__ __forceinline__ fp2p_t fp2_conj(const fp2p_t& a) { return pr_make(fp_sel(pr_odd(), fp_neg(a.v), a.v)); }
 // xi = 1 + u:  (a0 - a1) + (a0 + a1) u -- lane 0: a0 + (2q - a1), lane 1: a1 + a0
@@ -150,10 +159,27 @@ __device__ __forceinline__ fp2p_t fp2_sub2(const fp2p_t& a, const fp2p_t& b, con
 }
 __device__ __forceinline__ fp2p_t fp2_3m2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3m2(X.v, x.v)); }
 __device__ __forceinline__ fp2p_t fp2_3p2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3p2(X.v, x.v)); }
+#if BLS_FP2_INLINE == 2
+// inlined bodies fenced by scheduling barriers: the scheduler cannot interleave
+// two products, so the live set stays one product's temporaries + the caller's state
+__device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
+  BLS_PHASE();
+  const fp_t r = fp2p_mul_body(a.v, b.v);
+  BLS_PHASE();
+  return pr_make(r);
+}
+__device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) {
+  BLS_PHASE();
+  const fp_t r = fp2p_sqr_body(a.v);
+  BLS_PHASE();
+  return pr_make(r);
+}
+#else
 __device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
   return pr_make(fp_unpack(fp2p_mul_call(fp_pack(a.v), fp_pack(b.v))));
 }
 __device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) { return pr_make(fp_unpack(fp2p_sqr_call(fp_pack(a.v)))); }
+#endif
 __device__ __forceinline__ bool fp2_is_zero(const fp2p_t& a) { return pr_both(fp_is_zero(a.v)); }
 __device__ __forceinline__ bool fp2_eq(const fp2p_t& a, const fp2p_t& b) { return pr_both(fp_eq(a.v, b.v)); }
 

@@ -194,14 +194,14 @@ int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t mlen, const uint
   int np = 0;
   if (ss == PT_OK) {
     Q[np] = S;
-    Pa[np].x = G1_GEN_X_M;
-    Pa[np].y = G1_GEN_NEGY_M;
+    Pa[np].x = G1_VGEN_X_M;   // -[3(x^2-1)] g1, paired with the signature (k_hash_g2)
+    Pa[np].y = G1_VGEN_NEGY_M;
     ++np;
   }
   if (sp == PT_OK) {
     aff_t<fp2_t> c;
     hash_to_g2_candidate(c, msg, mlen, dom8);
-    if (jac_to_aff(Q[np], g2_mul_cofactor(c))) { Pa[np] = P; ++np; }
+    if (jac_to_aff(Q[np], g2_mul_bp(c))) { Pa[np] = P; ++np; }
   }
   return verify_pairs(np, Q, Pa);
 }
@@ -229,14 +229,14 @@ int hc_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, uint32
     if (!jac_to_aff(a, g.second)) continue;
     aff_t<fp2_t> c, h;
     hash_to_g2_candidate(c, (const uint8_t*)g.first.data(), mlen, dom8);
-    if (!jac_to_aff(h, g2_mul_cofactor(c))) continue;
+    if (!jac_to_aff(h, g2_mul_bp(c))) continue;
     Q.push_back(h);
     Pa.push_back(a);
   }
   if (ss == PT_OK) {
     aff_t<fp_t> ng;
-    ng.x = G1_GEN_X_M;
-    ng.y = G1_GEN_NEGY_M;
+    ng.x = G1_VGEN_X_M;
+    ng.y = G1_VGEN_NEGY_M;
     Q.push_back(S);
     Pa.push_back(ng);
   }
@@ -296,12 +296,12 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   g_fp_mul_count = 0;
   aff_t<fp2_t> c;
   hash_to_g2_candidate(c, msg32, 32, dom8);
-  jac_to_aff(H, g2_mul_cofactor(c));
+  jac_to_aff(H, g2_mul_bp(c));
   out[2] = g_fp_mul_count;
   if (sp != PT_OK || ss != PT_OK) { out[3] = out[4] = 0; return -1; }
   g_fp_mul_count = 0;
   aff_t<fp2_t> Q[2] = {S, H};
-  aff_t<fp_t> ng; ng.x = G1_GEN_X_M; ng.y = G1_GEN_NEGY_M;
+  aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
   g1_line_pre Pp[2] = {g1_prepare(ng), g1_prepare(P)};
   bool degen = false;
   const fp12_t f = miller_loop_n<2>(Q, Pp, degen);

@@ -476,16 +476,25 @@ def map_candidate(message_hash, dom8: bytes):
         x = add2(x, ONE2)
 
 
-def clear_cofactor_h2(P):
-    """[h2]P exactly, via [c^-1 mod r] BP(P) with c = 3(x^2-1) (device g2_mul_cofactor)."""
+def g2_bp(P):
+    """Budroni-Pintore BP(P) = [x^2-x-1]P + [x-1]psi(P) + psi^2(2P) = [3(x^2-1) h2]P
+    (device g2_mul_bp: the verification hash of the verify kernels)."""
     X = X_ABS
-    e0 = (X + 1) // 3
     F = Fq2
     neg = lambda p: jac_neg(F, p)
     add = lambda a, b: jac_add(F, a, b)
     t1 = jac_mul(F, P, X)
     Q0 = add(add(add(jac_mul(F, t1, X), t1), neg(P)), psi_jac(add(neg(t1), neg(P))))
-    Q0 = add(Q0, psi_jac(psi_jac(jac_dbl(F, P))))
+    return add(Q0, psi_jac(psi_jac(jac_dbl(F, P))))
+
+
+def clear_cofactor_h2(P):
+    """[h2]P exactly, via [c^-1 mod r] BP(P) with c = 3(x^2-1) (device g2_mul_cofactor)."""
+    e0 = (X_ABS + 1) // 3
+    F = Fq2
+    neg = lambda p: jac_neg(F, p)
+    add = lambda a, b: jac_add(F, a, b)
+    Q0 = g2_bp(P)
     Q1 = neg(psi_jac(Q0))
     Q2 = neg(psi_jac(Q1))
     T = add(add(jac_dbl(F, Q2), Q1), neg(psi_jac(Q2)))

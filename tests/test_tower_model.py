@@ -71,6 +71,44 @@ def test_cofactor_clearing_identity():
     assert k == e0 + (2 * e0 - 1) * M.X_ABS + (2 * e0 - 2) * M.X_ABS ** 2 + (e0 - 1) * M.X_ABS ** 3
 
 
+def _header_fp(name):
+    """A Montgomery-form fp_t constant of bls381_consts.hpp as an integer."""
+    import os
+    import re
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "consensus-specs_amd", "csrc", "bls381_consts.hpp")
+    m = re.search(r"fp_t %s = \{\{([^}]*)\}\}" % name, open(path).read())
+    limbs = [int(w.strip().rstrip("u"), 16) for w in m.group(1).split(",")]
+    v = sum(l << (28 * i) for i, l in enumerate(limbs))
+    return v * pow(2, -392, q) % q
+
+
+def test_verification_hash_scaling():
+    """The verify kernels pair BP(H0) = [c h2]H0 with the pubkey and the signature with
+    -[c]g1 (G1_VGEN_*), c = 3(x^2-1): the pairing product is the original one to the
+    power c, coprime to r, so the verdict is unchanged (bls381_hash.hpp g2_mul_bp)."""
+    F = M.Fq2
+    c = 3 * (M.X_ABS ** 2 - 1)
+    assert c % O.r and O.r % 3
+    cg = O.pt_normalize(O.FqOps, O.pt_multiply(O.FqOps, O.G1, c % O.r))
+    assert _header_fp("G1_VGEN_X_M") == cg[0] and _header_fp("G1_VGEN_NEGY_M") == (-cg[1]) % q
+    ncg = (cg[0], (-cg[1]) % q)
+    sk, msg, dom8 = 0x1234567, b"\x5a" * 32, (3).to_bytes(8, "big")
+    x, y = M.map_candidate(msg, dom8)
+    H0 = (x, y, M.ONE2)
+    bp = M.jac_to_affine(F, M.g2_bp(H0))
+    assert bp == M.jac_to_affine(F, M.jac_mul(F, M.clear_cofactor_h2(H0), c))
+    H = M.jac_to_affine(F, M.clear_cofactor_h2(H0))
+    pk = O.pt_normalize(O.FqOps, O.pt_multiply(O.FqOps, O.G1, sk))
+    sig = O.pt_normalize(O.Fq2Ops, O.pt_multiply(O.Fq2Ops, (H[0], H[1], M.ONE2), sk))
+    f_scaled = M.final_exp(M.miller_loop_multi([(sig, ncg), (bp, pk)]))
+    assert f_scaled == M.ONE12
+    pk2 = O.pt_normalize(O.FqOps, O.pt_multiply(O.FqOps, O.G1, sk + 1))
+    ng = (O.g_x, (-O.g_y) % q)
+    f_plain = M.final_exp(M.miller_loop_multi([(sig, ng), (H, pk2)]))
+    assert M.final_exp(M.miller_loop_multi([(sig, ncg), (bp, pk2)])) == M.pow12(f_plain, c % O.r) != M.ONE12
+
+
 def test_hash_sqrt_subgroup_models():
     rng = random.Random(4)
     for i in range(60):
