@@ -19,6 +19,13 @@ inline thread_local uint64_t g_fp_mul_count = 0;
 #else
 #define BLS_COUNT_FP_MUL() ((void)0)
 #endif
+#if !defined(__HIP_DEVICE_COMPILE__) && !defined(__HIP__)
+// host build: inversions that took fp_inv's fallback (tests assert none do)
+inline uint64_t g_inv_fallbacks = 0;
+#define BLS_COUNT_INV_FALLBACK() (++g_inv_fallbacks)
+#else
+#define BLS_COUNT_INV_FALLBACK() ((void)0)
+#endif
 
 // ----------------------------------------------------------------- Fp -----
 // Invariant for every fp_t crossing a function boundary: limbs < 2^28
@@ -335,7 +342,7 @@ BLS_HD inline fp_t fp_pow_qm3d4(const fp_t& a) {
   return r;
 }
 
-// (fp_inv: binary extended gcd, below the word helpers)
+// (fp_inv: optimized binary GCD, below the word helpers)
 BLS_HD inline fp_t fp_inv(const fp_t& a);
 
 // returns true and sets r when a is a square; r = a^((q+1)/4)
@@ -577,12 +584,12 @@ BLS_INLINE fp_t fp_from_words(const uint32_t w[12]) {
   return r;
 }
 
-// 1/a (0 -> 0).  Binary extended gcd on the integer A = aR mod q, the same loop
-// shape as fp_legendre (one subtraction, a conditional swap, one strip of twos
-// per step, ~270 steps of ~150 word ops), then A^-1 R^3 R^-1 = a^-1 R by one
-// Montgomery product.  Several times cheaper than a^(q-2) (453 Fp products).
+// 1/a (0 -> 0), variable-time binary extended gcd on the integer A = aR mod q
+// (one subtraction, a conditional swap, one strip of twos per step, ~270 steps
+// of ~150 word ops, the slowest lane of a wave setting the count), then
+// A^-1 R^3 R^-1 = a^-1 R by one Montgomery product.  The safety net of fp_inv.
 // Invariants: x1 A = u, x2 A = v (mod q); u, v odd after each strip; x1, x2 < 2q.
-BLS_HD inline fp_t fp_inv(const fp_t& am) {
+BLS_HD inline fp_t fp_inv_xgcd(const fp_t& am) {
   uint32_t u[12], v[12], x1[12], x2[12];
   fp_plain_to_words(u, fp_reduce_once(am));
   uint32_t z = 0;
@@ -621,6 +628,173 @@ BLS_HD inline fp_t fp_inv(const fp_t& am) {
 #pragma unroll
   for (int i = 0; i < 12; ++i) x1[i] = bq ? x1[i] : e[i];
   return fp_mul(fp_from_words(x1), FP_R3);
+}
+
+// ------------------------------- inversion (optimized binary GCD, Pornin) --
+// 1/a (0 -> 0) by the optimized binary GCD of T. Pornin ("Optimized Binary GCD
+// for Modular Inversion", 2020): a = A (the integer aR mod q), b = q, with
+// a = u A and b = v A (mod q) throughout.  Each of 26 outer rounds runs 30
+// binary-GCD steps on 62-bit approximations of a and b (their low 30 bits and
+// their top 32 bits at the common length), collecting the steps in a 2x2 matrix
+// (|f| + |g| <= 2^30), then applies it to the full values:
+//   a, b <- (f0 a + g0 b) / 2^30, (f1 a + g1 b) / 2^30     (exact; signs fixed)
+//   u, v <- (f0 u + g0 v) / 2^30, (f1 u + g1 v) / 2^30     (mod q, Montgomery-style)
+// 26 x 30 = 780 >= 2 len(q) - 1 steps bring b to gcd = 1 and v to A^-1.  Every
+// lane runs the same instruction stream (no data-dependent trip count), and a
+// value is 13 signed 30-bit limbs, so the matrix products are 32x32 -> 64-bit
+// multiply-adds with signed carries.  If b != 1 at the end (not expected: the
+// step bound is the paper's), the wave falls back to fp_inv_xgcd.
+constexpr int INV_L = 13;                 // 30-bit limbs
+constexpr uint32_t INV_M30 = (1u << 30) - 1;
+
+BLS_INLINE void inv_to_l30(int32_t r[INV_L], const uint32_t w[12]) {
+#pragma unroll
+  for (int k = 0; k < INV_L; ++k) {
+    const int bit = 30 * k, i = bit / 32, sh = bit % 32;
+    uint64_t v = (uint64_t)w[i] >> sh;
+    if (i + 1 < 12) v |= (uint64_t)w[i + 1] << (32 - sh);
+    r[k] = (int32_t)((uint32_t)v & INV_M30);
+  }
+}
+
+// (f x + g y) / 2^30 for x, y of 13 limbs (exact division: the low limb cancels);
+// the result's limbs are normalized (30 bits) except the top one, which is signed
+BLS_INLINE void inv_lin_shift(int32_t r[INV_L], const int32_t x[INV_L], const int32_t y[INV_L], int32_t f, int32_t g) {
+  int64_t acc = (int64_t)f * x[0] + (int64_t)g * y[0];
+  acc >>= 30;
+#pragma unroll
+  for (int i = 1; i < INV_L; ++i) {
+    acc += (int64_t)f * x[i] + (int64_t)g * y[i];
+    r[i - 1] = (int32_t)((uint32_t)acc & INV_M30);
+    acc >>= 30;
+  }
+  r[INV_L - 1] = (int32_t)acc;
+}
+
+// (f x + g y) / 2^30 mod q for x, y in [0, q): one Montgomery-style step with the
+// low limb's multiple of q, then the result in (-q, 2q) is brought into [0, q)
+BLS_INLINE void inv_lin_modq(int32_t r[INV_L], const int32_t x[INV_L], const int32_t y[INV_L], int32_t f, int32_t g) {
+  const int64_t lo = (int64_t)f * x[0] + (int64_t)g * y[0];
+  const int32_t k = (int32_t)(((uint32_t)lo * Q_NINV32) & INV_M30);
+  int64_t acc = lo + (int64_t)k * Q_L30[0];
+  acc >>= 30;
+#pragma unroll
+  for (int i = 1; i < INV_L; ++i) {
+    acc += (int64_t)f * x[i] + (int64_t)g * y[i] + (int64_t)k * Q_L30[i];
+    r[i - 1] = (int32_t)((uint32_t)acc & INV_M30);
+    acc >>= 30;
+  }
+  r[INV_L - 1] = (int32_t)acc;
+  // r in (-q, 2q): add q when negative, then subtract q when >= q
+  const int32_t addq = r[INV_L - 1] < 0 ? 1 : 0;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) {
+    const int32_t t = r[i] + (addq ? Q_L30[i] : 0) + c;
+    r[i] = (i < INV_L - 1) ? (int32_t)((uint32_t)t & INV_M30) : t;
+    c = t >> 30;
+  }
+  int32_t d[INV_L];
+  c = 0;
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) {
+    const int32_t t = r[i] - Q_L30[i] + c;
+    d[i] = (i < INV_L - 1) ? (int32_t)((uint32_t)t & INV_M30) : t;
+    c = t >> 30;
+  }
+  const bool ge = d[INV_L - 1] >= 0;
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) r[i] = ge ? d[i] : r[i];
+}
+
+// x <- -x (limbs normalized, top limb signed)
+BLS_INLINE void inv_neg(int32_t x[INV_L]) {
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) {
+    const int32_t t = c - x[i];
+    x[i] = (i < INV_L - 1) ? (int32_t)((uint32_t)t & INV_M30) : t;
+    c = t >> 30;
+  }
+}
+
+BLS_HD inline fp_t fp_inv(const fp_t& am) {
+  uint32_t w[12];
+  fp_plain_to_words(w, fp_reduce_once(am));
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) z |= w[i];
+  if (z == 0) return fp_zero();
+  int32_t a[INV_L], b[INV_L], u[INV_L], v[INV_L];
+  inv_to_l30(a, w);
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) { b[i] = Q_L30[i]; u[i] = 0; v[i] = 0; }
+  u[0] = 1;
+  for (int round = 0; round < 26; ++round) {
+    // approximations: low 30 bits, and the 32 bits below the common length n >= 62
+    int t = 2;
+    uint32_t top = 0;
+#pragma unroll
+    for (int i = 2; i < INV_L; ++i) {
+      const uint32_t c = (uint32_t)(a[i] | b[i]);
+      if (c) { t = i; top = c; }
+    }
+    const int bl = top ? 32 - __builtin_clz(top) : 2;   // bits of the top limb (n = 30 t + bl)
+    uint32_t a2 = 0, a1 = 0, a0 = 0, b2 = 0, b1 = 0, b0 = 0;
+#pragma unroll
+    for (int i = 2; i < INV_L; ++i) {
+      const bool s = i == t;
+      a2 = s ? (uint32_t)a[i] : a2; a1 = s ? (uint32_t)a[i - 1] : a1; a0 = s ? (uint32_t)a[i - 2] : a0;
+      b2 = s ? (uint32_t)b[i] : b2; b1 = s ? (uint32_t)b[i - 1] : b1; b0 = s ? (uint32_t)b[i - 2] : b0;
+    }
+    const uint64_t wa = ((uint64_t)a2 << 31) | ((uint64_t)a1 << 1) | (a0 >> 29);
+    const uint64_t wb = ((uint64_t)b2 << 31) | ((uint64_t)b1 << 1) | (b0 >> 29);
+    uint64_t xa = ((wa >> (bl - 1)) << 30) | (uint32_t)a[0];
+    uint64_t xb = ((wb >> (bl - 1)) << 30) | (uint32_t)b[0];
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 10
+    for (int j = 0; j < 30; ++j) {
+      const bool odd = (xa & 1) != 0;
+      const bool sw = odd && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xa = (odd ? ta - tb : ta) >> 1;
+      xb = tb;
+      f0 = odd ? tf0 - tf1 : tf0;
+      g0 = odd ? tg0 - tg1 : tg0;
+      f1 = tf1 + tf1;
+      g1 = tg1 + tg1;
+    }
+    int32_t na[INV_L], nb[INV_L];
+    inv_lin_shift(na, a, b, f0, g0);
+    inv_lin_shift(nb, a, b, f1, g1);
+    if (na[INV_L - 1] < 0) { inv_neg(na); f0 = -f0; g0 = -g0; }
+    if (nb[INV_L - 1] < 0) { inv_neg(nb); f1 = -f1; g1 = -g1; }
+    int32_t nu[INV_L], nv[INV_L];
+    inv_lin_modq(nu, u, v, f0, g0);
+    inv_lin_modq(nv, u, v, f1, g1);
+#pragma unroll
+    for (int i = 0; i < INV_L; ++i) { a[i] = na[i]; b[i] = nb[i]; u[i] = nu[i]; v[i] = nv[i]; }
+  }
+  uint32_t bad = (uint32_t)b[0] ^ 1u;
+#pragma unroll
+  for (int i = 1; i < INV_L; ++i) bad |= (uint32_t)b[i];
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) bad |= (uint32_t)a[i];
+  if (BLS_ANY(bad != 0)) {
+    BLS_COUNT_INV_FALLBACK();
+    return fp_inv_xgcd(am);
+  }
+  // v = A^-1 (canonical, 30-bit limbs) -> 28-bit limbs, then A^-1 R^3 / R
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int bit = 28 * k, i = bit / 30, sh = bit % 30;
+    uint64_t x = (uint64_t)(uint32_t)v[i] >> sh;
+    if (i + 1 < INV_L) x |= (uint64_t)(uint32_t)v[i + 1] << (30 - sh);
+    r.w[k] = (uint32_t)x & FP_MASK;
+  }
+  return fp_mul(r, FP_R3);
 }
 
 // ---------------------------------------------------------------- Fp2 -----
@@ -858,6 +1032,18 @@ BLS_INLINE bool fp12_eq(const fp12_g<E>& a, const fp12_g<E>& b) {
          fp2_eq(a.c1.c0, b.c1.c0) && fp2_eq(a.c1.c1, b.c1.c1) && fp2_eq(a.c1.c2, b.c1.c2);
 }
 
+template <class E>
+BLS_INLINE fp12_g<E> fp12_mul_inl(const fp12_g<E>& a, const fp12_g<E>& b) {
+  const fp6_g<E> ac = fp6_mul_inl(a.c0, b.c0);
+  const fp6_g<E> bd = fp6_mul_inl(a.c1, b.c1);
+  fp12_g<E> r;
+  r.c1 = fp6_sub2(fp6_mul_inl(fp6_add(a.c0, a.c1), fp6_add(b.c0, b.c1)), ac, bd);
+  r.c0 = fp6_add_mul_by_v(ac, bd);
+  return r;
+}
+
+// call version (loops of products, e.g. the segmented Fp12 products): its 84-word
+// operands go through the stack, so the final exponentiation inlines instead
 template <class E>
 BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
   const fp6_g<E> ac = fp6_mul(a.c0, b.c0);

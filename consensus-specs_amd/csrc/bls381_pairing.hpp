@@ -209,7 +209,7 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
     const E is = s ? fp2_mul(inv, pre[s - 1]) : inv;
     if (s) inv = fp2_mul(inv, fp2_mul_small(snap[s].g2, 4));
     const fp12_g<E> x = cyc_decompress(snap[s], is);
-    r = (s == 5) ? x : fp12_mul(r, x);
+    r = (s == 5) ? x : fp12_mul_inl(r, x);
   }
   return fp12_conj(r);
 }
@@ -219,15 +219,15 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
 // Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3.
 template <class E>
 BLS_HD inline fp12_g<E> final_exp(const fp12_g<E>& f) {
-  fp12_g<E> t = fp12_mul(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
-  t = fp12_mul(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
-  fp12_g<E> a = fp12_mul(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
-  a = fp12_mul(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
-  const fp12_g<E> b = fp12_mul(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
+  fp12_g<E> t = fp12_mul_inl(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
+  t = fp12_mul_inl(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
+  fp12_g<E> a = fp12_mul_inl(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
+  a = fp12_mul_inl(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
+  const fp12_g<E> b = fp12_mul_inl(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
   const fp12_g<E> bx2 = cyc_exp_x(cyc_exp_x(b));
-  const fp12_g<E> c = fp12_mul(fp12_mul(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
-  const fp12_g<E> t3 = fp12_mul(fp12_cyclotomic_sqr(t), t);
-  return fp12_mul(c, t3);
+  const fp12_g<E> c = fp12_mul_inl(fp12_mul_inl(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
+  const fp12_g<E> t3 = fp12_mul_inl(fp12_cyclotomic_sqr(t), t);
+  return fp12_mul_inl(c, t3);
 }
 
 }  // namespace bls381

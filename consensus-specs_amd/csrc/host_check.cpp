@@ -68,6 +68,8 @@ void hc_fp_add(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_add(ld
 void hc_fp_sub(const uint8_t* a, const uint8_t* b, uint8_t* o) { st(o, fp_sub(ld(a), ld(b))); }
 void hc_fp_half(const uint8_t* a, uint8_t* o) { st(o, fp_half(ld(a))); }
 void hc_fp_inv(const uint8_t* a, uint8_t* o) { st(o, fp_inv(ld(a))); }
+void hc_fp_inv_xgcd(const uint8_t* a, uint8_t* o) { st(o, fp_inv_xgcd(ld(a))); }
+uint64_t hc_inv_fallbacks() { return g_inv_fallbacks; }
 int hc_fp_sqrt(const uint8_t* a, uint8_t* o) {
   fp_t r;
   const bool ok = fp_sqrt(r, ld(a));

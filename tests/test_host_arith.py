@@ -287,19 +287,30 @@ def test_scalar_mul_fixture_helpers(L):
     assert out.raw == O.privtopub(k)
 
 
-def test_fp_inv_binary_xgcd_edges(L):
-    """fp_inv (binary extended gcd on the Montgomery integer): random values and values whose
-    Montgomery form has long runs of factors of two or sits next to q; 0 -> 0."""
+def test_fp_inv_binary_gcd_edges(L):
+    """fp_inv (Pornin's optimized binary GCD on the Montgomery integer) and its fallback
+    fp_inv_xgcd: random values, Montgomery integers with long runs of factors of two, small,
+    near q, near powers of two, all-ones patterns; 0 -> 0.  The fast path must finish every
+    one of them (no fallback taken)."""
     R = 1 << 392
     rinv = pow(R, -1, q)
     rng = random.Random(61)
     buf = ctypes.create_string_buffer(48)
+    L.hc_inv_fallbacks.restype = ctypes.c_uint64
+    before = L.hc_inv_fallbacks()
     vals = [1, 2, q - 1, q - 2, (q + 1) // 2, 3]
-    # a whose Montgomery integer aR mod q is 2^k (k up to 380, including >= 32 zero low bits)
-    vals += [(1 << k) * rinv % q for k in (1, 31, 32, 33, 64, 100, 200, 380)]
-    vals += [rng.randrange(1, q) for _ in range(1500)]
+    mont = [1 << k for k in range(381)] + [q - (1 << k) for k in range(381)]
+    mont += [(1 << k) - 1 for k in range(2, 382)] + [(1 << k) + 1 for k in range(2, 381)]
+    mont += list(range(1, 300)) + [q - k for k in range(1, 300)] + [q // 3, q // 5, (q - 1) // 2]
+    mont += [rng.randrange(1, 1 << rng.randrange(2, 381)) for _ in range(3000)]
+    vals += [(m % q) * rinv % q for m in mont if m % q]
+    vals += [rng.randrange(1, q) for _ in range(6000)]
     for a in vals:
         L.hc_fp_inv(b48(a), buf)
         assert i48(buf.raw) * a % q == 1, a
+    for a in vals[:300]:
+        L.hc_fp_inv_xgcd(b48(a), buf)
+        assert i48(buf.raw) * a % q == 1, a
+    assert L.hc_inv_fallbacks() == before
     L.hc_fp_inv(b48(0), buf)
     assert i48(buf.raw) == 0
