@@ -38,7 +38,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
 
-VALU_PEAK_FILE = os.path.join(ROOT, "profiles", "valu_peak_r01.json")
+VALU_PEAK_FILE = os.path.join(ROOT, "profiles", "valu_peak_r02.json")
 # Algorithmic work unit: one 381-bit Montgomery product = 300 32x32->64 MACs
 # (12x12 product + 12x12 reduction + 12 quotient digits at 32-bit limbs).  The
 # engine's radix-2^28 product issues 392 MACs; the excess is implementation

@@ -50,6 +50,35 @@ __global__ void __launch_bounds__(128, 2) k_fp2mul(size_t nl, int reps, const ui
   for (int i = 0; i < reps; ++i) x = fp2_mul(x, y);
   st(out, nl, lane, 0, x.v);
 }
+// two independent products per step, bodies inlined (ILP inside one call boundary)
+__global__ void __launch_bounds__(128, 2) k_fp2mul_x2(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  fp_t x = ld(in, nl, lane, 0), y = ld(in, nl, lane, 1), z = ld(in, nl, lane, 2), w = ld(in, nl, lane, 3);
+  for (int i = 0; i < reps; i += 2) {
+    x = fp2p_mul_body(x, y);
+    z = fp2p_mul_body(z, w);
+  }
+  st(out, nl, lane, 0, x); st(out, nl, lane, 1, z);
+}
+// the call loop at 3 and 4 waves per SIMD
+__global__ void __launch_bounds__(128, 3) k_fp2mul_o3(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  fp2p_t x = pr_make(ld(in, nl, lane, 0)), y = pr_make(ld(in, nl, lane, 1));
+  for (int i = 0; i < reps; ++i) x = fp2_mul(x, y);
+  st(out, nl, lane, 0, x.v);
+}
+__global__ void __launch_bounds__(128, 4) k_fp2mul_o4(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  fp2p_t x = pr_make(ld(in, nl, lane, 0)), y = pr_make(ld(in, nl, lane, 1));
+  for (int i = 0; i < reps; ++i) x = fp2_mul(x, y);
+  st(out, nl, lane, 0, x.v);
+}
+__global__ void __launch_bounds__(128, 1) k_fp2mul_o1(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  fp2p_t x = pr_make(ld(in, nl, lane, 0)), y = pr_make(ld(in, nl, lane, 1));
+  for (int i = 0; i < reps; ++i) x = fp2_mul(x, y);
+  st(out, nl, lane, 0, x.v);
+}
 __global__ void __launch_bounds__(128, 2) k_fp2sqr(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
   KHEAD
   fp2p_t x = pr_make(ld(in, nl, lane, 0));
@@ -162,6 +191,10 @@ int main(int argc, char** argv) {
   const Bench B[] = {
       {"fp_mul (one lane)", k_fpmul, 256, "op"},
       {"fp2_mul (pair)", k_fp2mul, 256, "op"},
+      {"fp2_mul x2 inlined (pair)", k_fp2mul_x2, 256, "op"},
+      {"fp2_mul 1 wave/SIMD (pair)", k_fp2mul_o1, 256, "op"},
+      {"fp2_mul 3 waves/SIMD (pair)", k_fp2mul_o3, 256, "op"},
+      {"fp2_mul 4 waves/SIMD (pair)", k_fp2mul_o4, 256, "op"},
       {"fp2_sqr (pair)", k_fp2sqr, 256, "op"},
       {"fp2_add_mul_xi (pair)", k_fp2add, 1024, "op"},
       {"fp_inv (xgcd)", k_inv, 8, "op"},

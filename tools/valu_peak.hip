@@ -82,6 +82,53 @@ __global__ __launch_bounds__(256) void k_add(uint64_t* out, uint32_t seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// one instruction template per kernel: 8 independent chains of 32-bit values
+#define K32(NAME, ASM, ...)                                                               \
+  __global__ __launch_bounds__(256) void NAME(uint64_t* out, uint32_t seed) {             \
+    uint32_t a = seed + threadIdx.x, b = seed * 7u + 3u;                                  \
+    uint32_t x[8];                                                                        \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) x[k] = a + k;                          \
+    for (int i = 0; i < ITERS; ++i) {                                                     \
+      _Pragma("unroll") for (int k = 0; k < 8; ++k) asm volatile(ASM : "+v"(x[k]) : "v"(a), "v"(b) __VA_ARGS__); \
+    }                                                                                     \
+    uint64_t s = 0;                                                                       \
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) s ^= x[k];                             \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                       \
+  }
+K32(k_alignbit, "v_alignbit_b32 %0, %1, %0, 28")
+K32(k_add3, "v_add3_u32 %0, %0, %1, %2")
+K32(k_and, "v_and_b32 %0, %0, %1")
+K32(k_cndmask, "v_cmp_lt_u32 vcc, %1, %2\n\tv_cndmask_b32 %0, %0, %1, vcc", : "vcc")
+K32(k_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K32(k_lshl_add, "v_lshl_add_u32 %0, %0, 4, %1")
+// 64-bit shift / shift-add on 8 independent 64-bit chains
+__global__ __launch_bounds__(256) void k_shr64(uint64_t* out, uint32_t seed) {
+  uint64_t x[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = ((uint64_t)(seed + k) << 40) | threadIdx.x;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(x[k]));
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ __launch_bounds__(256) void k_lshladd64(uint64_t* out, uint32_t seed) {
+  uint64_t x[8], y = ((uint64_t)seed << 20) | threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = ((uint64_t)(seed + k) << 30) | threadIdx.x;
+  for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(x[k]) : "v"(y));
+  }
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s ^= x[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <typename K>
 static double time_kernel(K kern, uint64_t* d, int blocks, int reps) {
   hipEvent_t e0, e1;
@@ -113,6 +160,22 @@ int main() {
   printf(", \"v_mul_lo_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
   t = time_kernel(k_add, d, blocks, 5);
   printf(", \"v_add_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_alignbit, d, blocks, 5);
+  printf(", \"v_alignbit_b32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_add3, d, blocks, 5);
+  printf(", \"v_add3_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_and, d, blocks, 5);
+  printf(", \"v_and_b32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_cndmask, d, blocks, 5);
+  printf(", \"v_cmp+v_cndmask_Tops\": %.3f", 2.0 * ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_dpp, d, blocks, 5);
+  printf(", \"v_mov_b32_dpp_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_lshl_add, d, blocks, 5);
+  printf(", \"v_lshl_add_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_shr64, d, blocks, 5);
+  printf(", \"v_lshrrev_b64_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  t = time_kernel(k_lshladd64, d, blocks, 5);
+  printf(", \"v_lshl_add_u64_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
   printf("}\n");
   CHECK(hipFree(d));
   return 0;
