@@ -193,13 +193,42 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
     if (rc__) return rc__;                                          \
   } while (0)
 
+// final exponentiation + verdict of n Fp12 values (lane-pair SoA): on lane quads while
+// the batch leaves SIMDs idle (k_final_exp_verdict_q: half the per-item latency, more
+// lane work), on lane pairs above that
+#ifndef BLS_FE_QUAD_MAX_N
+#define BLS_FE_QUAD_MAX_N 16384
+#endif
+int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts) {
+  if (n <= BLS_FE_QUAD_MAX_N)
+    LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), dim3(KBLOCK), k_final_exp_verdict_q<1>, n, f, st, verdicts);
+  else
+    LAUNCH("final_exp", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_final_exp_verdict, n, f, st, verdicts);
+  return 0;
+}
+#define LAUNCH_FE(s, n, f, st, v)                                                                   \
+  do {                                                                                              \
+    int rc__ = launch_final_exp(s, n, (const uint32_t*)(f), (const uint8_t*)(st), v);               \
+    if (rc__) return rc__;                                                                          \
+  } while (0)
+
 // ----------------------------------------------------- verify_batch (C2) --
 struct VerifyWs {
   uint32_t *pk_aff, *sig_aff, *h_aff, *f;
   uint8_t *pk_st, *sig_st, *f_st;
 };
+// bls_verify batches of at most this many items run each Miller pair on its own lane
+// quad (k_miller_verify_o, 8 lanes per item: the lowest latency), up to
+// BLS_ML_QUAD_MAX_N both pairs of an item on one quad (k_miller_verify_q), above that
+// on lane pairs (k_miller_verify: the least work per item)
+#ifndef BLS_ML_OCT_MAX_N
+#define BLS_ML_OCT_MAX_N 8192
+#endif
+// Fp12 values the Miller stage of a verify batch writes (two per item on the octet path)
+size_t verify_nf(size_t n) { return n <= BLS_ML_OCT_MAX_N ? 2 * n : n; }
 size_t verify_ws_size(size_t n) {
-  return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * n) + 3 * align256(n) + 1024;
+  return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
+         align256(verify_nf(n)) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n) {
   Bump b(ws);
@@ -207,10 +236,10 @@ VerifyWs carve_verify(void* ws, size_t n) {
   w.pk_aff = b.take<uint32_t>(2 * FP_LIMBS * n);
   w.sig_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
   w.h_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
-  w.f = b.take<uint32_t>(12 * FP_LIMBS * n);
+  w.f = b.take<uint32_t>(12 * FP_LIMBS * verify_nf(n));
   w.pk_st = b.take<uint8_t>(n);
   w.sig_st = b.take<uint8_t>(n);
-  w.f_st = b.take<uint8_t>(n);
+  w.f_st = b.take<uint8_t>(verify_nf(n));
   return w;
 }
 
@@ -249,6 +278,15 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
 #endif
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (n <= BLS_ML_OCT_MAX_N) {
+    // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
+    LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
+           (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+           w.f, w.f_st);
+    LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), b, k_final_exp_verdict_q<2>, n, (const uint32_t*)w.f,
+           (const uint8_t*)w.f_st, verdicts);
+    return 0;
+  }
   if (n <= BLS_ML_QUAD_MAX_N) {
     // latency path: one item per lane quad, its two pairs side by side (half the per-item latency,
     // ~13% more work per item -- the better trade while the batch leaves SIMDs idle)
@@ -259,7 +297,7 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
            (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
   }
-  LAUNCH("final_exp", s, g2, b, k_final_exp_verdict, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts);
+  LAUNCH_FE(s, n, w.f, w.f_st, verdicts);
   return 0;
 }
 
@@ -368,6 +406,11 @@ int run_agg(const AggPlan& p, size_t ng, const uint8_t* d_in, void* ws, hipStrea
 // per call.
 constexpr int32_t PAIR_NONE = INT32_MIN;
 
+// verify_multiple batches of at most this many Miller pairs run one pair per lane quad
+// (the latency path of small batches: an epoch's attestations, single calls)
+#ifndef BLS_VM_TASK_MAX
+#define BLS_VM_TASK_MAX 8192
+#endif
 struct VmPlan {
   size_t n_calls = 0, n_keys = 0, G = 0, nquads = 0;
   std::vector<uint32_t> key_idx;        // caller key index of every group member, in group order
@@ -377,6 +420,10 @@ struct VmPlan {
   std::vector<int32_t> quad_pair;       // 2 per quad: group >= 0, -(call + 1) = the signature pair, or PAIR_NONE
   std::vector<uint32_t> call_quad_off;  // n_calls + 1 offsets into the quads
   std::vector<std::vector<agg_chunk>> passes;  // segmented Fp12 products (empty: one quad per call)
+  // latency path (small batches): one quad per Miller pair (k_miller_tasks_q1); the pair
+  // tasks are the quad_pair entries, and these passes multiply them per call
+  bool tasks = false;
+  std::vector<std::vector<agg_chunk>> task_passes;
   AggPlan agg;                                 // group pubkey sums over key_idx order
 };
 
@@ -415,6 +462,26 @@ bool is_inf_encoding(const uint8_t* b, size_t len) {
 }
 
 // h_pks / h_sigs may be NULL (device-resident keys / signatures: nothing is dropped)
+// 64-bit mix of a message (8-byte words, multiply-xorshift), for the grouping table
+uint64_t msg_hash(const uint8_t* m, size_t len) {
+  uint64_t h = 0x9e3779b97f4a7c15ull ^ len;
+  size_t i = 0;
+  for (; i + 8 <= len; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, m + i, 8);
+    h = (h ^ w) * 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 31;
+  }
+  uint64_t t = 0;
+  for (size_t k = 0; i + k < len; ++k) t |= (uint64_t)m[i + k] << (8 * k);
+  h = (h ^ t) * 0x94d049bb133111ebull;
+  return h ^ (h >> 29);
+}
+
+// Host plan of a verify_multiple batch: per call, pubkeys grouped by distinct message
+// (py_ecc's verify_multiple: groups in first-occurrence order, members in index order).
+// One flat open-addressing table (generation-stamped, reused across calls) and a
+// counting sort per call: linear in the number of keys.
 VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, size_t mlen, const uint8_t* h_pks,
                const uint8_t* h_sigs, const int* with_sig) {
   VmPlan pl;
@@ -422,32 +489,49 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, si
   pl.n_keys = call_off[n_calls];
   pl.group_off.push_back(0);
   pl.call_quad_off.push_back(0);
+  pl.key_idx.reserve(pl.n_keys);
+  size_t maxc = 0;
+  for (size_t c = 0; c < n_calls; ++c) maxc = std::max<size_t>(maxc, call_off[c + 1] - call_off[c]);
+  size_t cap = 16;
+  while (cap < 2 * maxc) cap <<= 1;
+  std::vector<uint32_t> slot(cap), stamp(cap, 0), gid(maxc), first, cnt, pos, flat(maxc);
+  std::vector<int32_t> pairs;
+  auto same = [&](uint32_t a, uint32_t b) { return mlen == 0 || std::memcmp(msgs + mlen * a, msgs + mlen * b, mlen) == 0; };
   for (size_t c = 0; c < n_calls; ++c) {
-    std::unordered_map<std::string, uint32_t> idx;
-    std::vector<std::vector<uint32_t>> members;
-    std::vector<uint32_t> first;
-    for (uint32_t i = call_off[c]; i < call_off[c + 1]; ++i) {
-      std::string key((const char*)msgs + mlen * i, mlen);
-      auto it = idx.find(key);
-      if (it == idx.end()) {
-        idx.emplace(key, (uint32_t)members.size());
-        members.push_back({i});
-        first.push_back(i);
-      } else {
-        members[it->second].push_back(i);
+    const uint32_t b0 = call_off[c], e0 = call_off[c + 1], gen = (uint32_t)c + 1;
+    first.clear();
+    cnt.clear();
+    for (uint32_t i = b0; i < e0; ++i) {
+      size_t h = mlen ? (size_t)msg_hash(msgs + mlen * (size_t)i, mlen) & (cap - 1) : 0;
+      while (true) {
+        if (stamp[h] != gen) {
+          stamp[h] = gen;
+          slot[h] = (uint32_t)first.size();
+          first.push_back(i);
+          cnt.push_back(0);
+          break;
+        }
+        if (same(first[slot[h]], i)) break;
+        h = (h + 1) & (cap - 1);
       }
+      gid[i - b0] = slot[h];
+      ++cnt[slot[h]];
     }
-    std::vector<int32_t> pairs;
-    for (size_t gi = 0; gi < members.size(); ++gi) {
-      const auto& m = members[gi];
+    const size_t ng = first.size();
+    pos.assign(ng + 1, 0);
+    for (size_t g = 0; g < ng; ++g) pos[g + 1] = pos[g] + cnt[g];
+    for (uint32_t i = b0; i < e0; ++i) flat[pos[gid[i - b0]]++] = i;   // pos[g] ends at group g's end
+    pairs.clear();
+    for (size_t g = 0; g < ng; ++g) {
+      const uint32_t* m = flat.data() + pos[g] - cnt[g];
       if (h_pks) {
         bool all_inf = true;
-        for (uint32_t i : m) all_inf = all_inf && is_inf_encoding(h_pks + 48 * (size_t)i, 48);
+        for (uint32_t k = 0; k < cnt[g] && all_inf; ++k) all_inf = is_inf_encoding(h_pks + 48 * (size_t)m[k], 48);
         if (all_inf) continue;
       }
-      pl.key_idx.insert(pl.key_idx.end(), m.begin(), m.end());
+      pl.key_idx.insert(pl.key_idx.end(), m, m + cnt[g]);
       pl.group_off.push_back((uint32_t)pl.key_idx.size());
-      pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * first[gi], msgs + mlen * (first[gi] + 1));
+      pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * first[g], msgs + mlen * (first[g] + 1));
       pl.group_call.push_back((uint32_t)c);
       pairs.push_back((int32_t)pl.G);
       ++pl.G;
@@ -462,6 +546,12 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, si
   }
   pl.nquads = pl.quad_pair.size() / 2;
   if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
+  if (2 * pl.nquads <= BLS_VM_TASK_MAX) {
+    pl.tasks = true;
+    std::vector<uint32_t> toff(pl.call_quad_off.size());
+    for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
+    pl.task_passes = plan_products(toff);
+  }
   if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
   return pl;
 }
@@ -524,6 +614,54 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
 
 // each lane multiplies one chunk [begin, end) of Fp12 values (statuses OR-ed);
 // an empty chunk yields 1 (the empty product of an empty call)
+// The latency form of k_miller_quads: pair task t (entry t of quad_pair) on lane
+// quad t, miller_loop_q1 (every step's products split over the halves).  Writes one
+// Fp12 (pair SoA over nt values) and status per task: PAIR_NONE or an infinite
+// operand is f = 1; a bad operand or a degenerate loop is ST_BAD.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1(size_t nt, const int32_t* __restrict__ tasks,
+                                                           size_t G, const uint32_t* __restrict__ h_aff,
+                                                           const uint8_t* __restrict__ h_st,
+                                                           const uint32_t* __restrict__ agg_aff,
+                                                           const uint8_t* __restrict__ agg_st, size_t ncalls,
+                                                           const uint32_t* __restrict__ sig_aff,
+                                                           const uint8_t* __restrict__ sig_st,
+                                                           uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t t = item_index<4>();
+  if (t >= nt) return;
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const int p = pr_odd() ? 1 : 0;
+  const int32_t src = tasks[t];
+  uint8_t sq = ST_INF, sp = ST_INF;
+  if (src >= 0) { sq = h_st[src]; sp = agg_st[src]; }
+  else if (src != PAIR_NONE) { sq = sig_st[(size_t)(-src - 1)]; sp = ST_OK; }
+  if (sq == ST_BAD || sp == ST_BAD) { if (lead) st_out[t] = ST_BAD; return; }
+  fq12_t f;
+  bool degen = false;
+  if (sq == ST_OK && sp == ST_OK) {
+    aff_t<fp2p_t> Q;
+    aff_t<fp_t> P;
+    if (src >= 0) {
+      Q.x = pr_make(soa_ld(h_aff, 2 * G, 2 * (size_t)src + p, 0));
+      Q.y = pr_make(soa_ld(h_aff, 2 * G, 2 * (size_t)src + p, 1));
+      P = soa_ld_g1(agg_aff, G, (size_t)src);
+    } else {
+      const size_t c = (size_t)(-src - 1);
+      Q.x = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 0));
+      Q.y = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 1));
+      P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
+    }
+    f = miller_loop_q1(Q, g1_prepare(P), degen);
+  } else {
+    f = fq12_one();
+  }
+  const size_t lp = 2 * t + p;
+  const int c0 = qd_hi() ? 3 : 0;
+  soa_st(f_out, 2 * nt, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * nt, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * nt, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
+}
+
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_chunk_product(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                               const uint32_t* __restrict__ in, size_t n_in,
                                                               const uint8_t* __restrict__ in_st,
@@ -612,14 +750,21 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   }
-  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nq);
-  uint8_t* st = b.take<uint8_t>(nq);
-  LAUNCH("miller_quads", s, dim3(grid_for(4 * nq)), dim3(KBLOCK), k_miller_quads, nq, (const int32_t*)d_qp, G,
-         (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
-         (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+  const size_t nf = pl.tasks ? 2 * nq : nq;
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nf);
+  uint8_t* st = b.take<uint8_t>(nf);
+  if (pl.tasks) {
+    LAUNCH("miller_tasks_q1", s, dim3(grid_for(4 * nf)), dim3(KBLOCK), k_miller_tasks_q1, nf, (const int32_t*)d_qp,
+           G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+  } else {
+    LAUNCH("miller_quads", s, dim3(grid_for(4 * nq)), dim3(KBLOCK), k_miller_quads, nq, (const int32_t*)d_qp, G,
+           (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+  }
   // segmented products (chunk lists live in the plan, which outlives the stream work)
-  size_t n_in = nq;
-  for (const auto& chunks : pl.passes) {
+  size_t n_in = nf;
+  for (const auto& chunks : pl.tasks ? pl.task_passes : pl.passes) {
     agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
     uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
     uint8_t* nst = b.take<uint8_t>(chunks.size());
@@ -644,8 +789,8 @@ size_t vm_ws_bound(const VmPlan& pl, size_t mlen) {
   s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
   s += agg_ws_size(pl.agg, 3) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
-  s += align256(12 * FPW * nq) + align256(nq);
-  for (const auto& ch : pl.passes)
+  s += align256(12 * FPW * 2 * nq) + align256(2 * nq);
+  for (const auto& ch : pl.tasks ? pl.task_passes : pl.passes)
     s += align256(ch.size() * sizeof(agg_chunk)) + align256(12 * FPW * ch.size()) + align256(ch.size());
   s += align256(nc);
   return s;
@@ -662,9 +807,11 @@ size_t vm_ws_bound_sizes(size_t n_calls, size_t n_keys, size_t mlen) {
   const size_t chunks = G + n_keys / CHUNK_L1 + 1;
   s += 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks)) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
-  s += align256(12 * FPW * nq) + align256(nq);
-  // product passes: <= nq / 8 + n_calls chunks per pass, and the sizes shrink 8x per pass
-  const size_t pc = nq / 4 + 2 * nc;
+  // Miller values: quads, or two pair tasks per quad on the latency path
+  s += align256(12 * FPW * 2 * nq) + align256(2 * nq);
+  // product passes: <= nt / 8 + n_calls chunks per pass over nt <= 2 nq values, and the
+  // sizes shrink 8x per pass
+  const size_t pc = nq / 2 + 2 * nc;
   s += 8 * (align256(pc * sizeof(agg_chunk)) + align256(12 * FPW * pc) + align256(pc));
   s += align256(nc);
   return s;
@@ -853,8 +1000,7 @@ int bls381_verify_multiple_batch(size_t n_calls, const uint32_t* call_off, const
   uint8_t* st;
   if ((rc = vm_host(c, n_calls, call_off, pks, msgs, msg_len, sigs, dom8s, with_sig.data(), b, &f, &st))) return rc;
   uint8_t* d_v = b.take<uint8_t>(n_calls);
-  LAUNCH("final_exp", c->stream, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls,
-         (const uint32_t*)f, (const uint8_t*)st, d_v);
+  LAUNCH_FE(c->stream, n_calls, f, st, d_v);
   HIPC(hipMemcpyAsync(verdicts, d_v, n_calls, hipMemcpyDeviceToHost, c->stream));
   HIPC(hipStreamSynchronize(c->stream));
   return 0;
@@ -887,8 +1033,7 @@ int bls381_verify_multiple_batch_device(size_t n_calls, const uint32_t* h_call_o
   uint32_t* f;
   uint8_t* st;
   if ((rc = run_vm_batch(c, *pl, msg_len, d_pks, d_sigs, d_dom8s, b, s, &f, &st))) return rc;
-  LAUNCH("final_exp", s, dim3(grid_for(2 * n_calls)), dim3(KBLOCK), k_final_exp_verdict, n_calls, (const uint32_t*)f,
-         (const uint8_t*)st, d_verdicts);
+  LAUNCH_FE(s, n_calls, f, st, d_verdicts);
   return keep_until_done(c, s, pl);   // the plan's arrays are async copy sources
 } catch (const std::exception& e) {
   t_err = e.what();
@@ -958,8 +1103,7 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) try {
     n_in = chunks.size();
   }
   uint8_t* d_v = b.take<uint8_t>(1);
-  LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)f,
-         (const uint8_t*)st, d_v);
+  LAUNCH_FE(s, (size_t)1, f, st, d_v);
   uint8_t v = 0;
   HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
@@ -1818,8 +1962,7 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
       gst = nst;
       n_in = chunks.size();
     }
-    LAUNCH("final_exp", s, dim3(1), dim3(KBLOCK), k_final_exp_verdict, (size_t)1, (const uint32_t*)g,
-           (const uint8_t*)gst, d_v);
+    LAUNCH_FE(s, (size_t)1, g, gst, d_v);
     if ((rc = keep_until_done(c, s, passes))) return rc;
   }
   if (!cm->virt) NCCLC(api, api->broadcast(d_v, d_v, 1, ncclUint8, 0, cm->comm, s));
@@ -2028,8 +2171,7 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     n_in = chunks.size();
   }
   uint8_t* bv = b.take<uint8_t>(nb);
-  LAUNCH("final_exp", s, dim3(grid_for(2 * nb)), blk, k_final_exp_verdict, nb, (const uint32_t*)f,
-         (const uint8_t*)fst, bv);
+  LAUNCH_FE(s, nb, f, fst, bv);
   std::vector<uint8_t> h_bv(nb), h_cls(n);
   HIPC(hipMemcpyAsync(h_bv.data(), bv, nb, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(h_cls.data(), cls, n, hipMemcpyDeviceToHost, s));

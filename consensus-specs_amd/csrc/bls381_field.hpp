@@ -153,6 +153,16 @@ BLS_INLINE fp_t fp_3p2(const fp_t& X, const fp_t& x) {
   for (int i = 0; i < 14; ++i) s[i] = 3u * X.w[i] + (x.w[i] << 1);
   return fp_reduce_lc<5>(s);
 }
+// 3X - 2x (minus) or 3X + 2x, chosen per lane (same bounds as fp_3m2 / fp_3p2)
+BLS_INLINE fp_t fp_3pm2(const fp_t& X, const fp_t& x, bool minus) {
+  uint32_t s[14];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const uint32_t x2 = x.w[i] << 1;
+    s[i] = 3u * X.w[i] + (minus ? Q4B_LIMBS[i] - x2 : x2);
+  }
+  return fp_reduce_lc<5>(s);
+}
 
 // lazy sum for a multiplication operand only: limbs < 2^29, value < 4q
 BLS_INLINE fp_t fp_add_lazy(const fp_t& a, const fp_t& b) {

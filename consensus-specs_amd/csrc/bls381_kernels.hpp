@@ -246,6 +246,50 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_q
   if (lead) st_out[i] = degen ? ST_BAD : ST_OK;
 }
 
+// The latency form of k_miller_verify: one quad per Miller pair (miller_loop_q1).
+// Pair task t = 2i + k of item i runs on lanes 4t..4t+3: k = 0 the pair
+// (sig, -[c]g1), k = 1 (BP(H0), pk).  Each task writes its own Fp12 (pair SoA over
+// 2n values) and status; an inactive pair (infinite operand) writes f = 1.
+// k_final_exp_verdict_q<2> multiplies the two.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_o(size_t n, const uint32_t* __restrict__ sig_aff,
+                                                           const uint8_t* __restrict__ sig_st,
+                                                           const uint32_t* __restrict__ pk_aff,
+                                                           const uint8_t* __restrict__ pk_st,
+                                                           const uint32_t* __restrict__ h_aff,
+                                                           uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t t = item_index<4>();
+  if (t >= 2 * n) return;
+  const size_t i = t >> 1;
+  const bool hpair = (t & 1) != 0;
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const int p = pr_odd() ? 1 : 0;
+  const uint8_t ss = sig_st[i], ps = pk_st[i];
+  if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[t] = ST_BAD; return; }
+  fq12_t f;
+  bool degen = false;
+  if (hpair ? ps == ST_OK : ss == ST_OK) {
+    const uint32_t* qsrc = hpair ? h_aff : sig_aff;
+    aff_t<fp2p_t> Q;
+    Q.x = pr_make(soa_ld(qsrc, 2 * n, 2 * i + p, 0));
+    Q.y = pr_make(soa_ld(qsrc, 2 * n, 2 * i + p, 1));
+    aff_t<fp_t> P;
+    if (hpair) {
+      P = soa_ld_g1(pk_aff, n, i);
+    } else {
+      P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
+    }
+    f = miller_loop_q1(Q, g1_prepare(P), degen);
+  } else {
+    f = fq12_one();
+  }
+  const size_t lp = 2 * t + p;
+  const int c0 = qd_hi() ? 3 : 0;
+  soa_st(f_out, 4 * n, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 4 * n, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 4 * n, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
+}
+
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {
@@ -255,6 +299,37 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   if (st[i] != ST_OK) { if (lead) verdict[i] = 0; return; }
   const fp12p_t f = soa_ld12(f_in, n, i);
   const bool one = fp12_is_one(final_exp(f));
+  if (lead) verdict[i] = one ? 1 : 0;
+}
+
+// The same verdict on a lane quad (final_exp_q: each half holds one Fp6 half of
+// f and runs half of every Fp12 step): half the per-item latency, for batches
+// that leave SIMDs idle.  Item i's f is the product of NF values NF i + k of the
+// pair-SoA layout k_final_exp_verdict reads (NF = 2: the two Miller pairs of
+// k_miller_verify_o); any value not ST_OK makes the verdict False.
+template <int NF>
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_q(size_t n, const uint32_t* __restrict__ f_in,
+                                                               const uint8_t* __restrict__ st,
+                                                               uint8_t* __restrict__ verdict) {
+  const size_t i = item_index<4>();
+  if (i >= n) return;
+  const bool lead = (threadIdx.x & 3u) == 0;
+  bool ok = true;
+  for (int k = 0; k < NF; ++k) ok = ok && st[NF * i + k] == ST_OK;
+  if (!ok) { if (lead) verdict[i] = 0; return; }
+  const int p = pr_odd() ? 1 : 0;
+  const int c0 = qd_hi() ? 3 : 0;
+  const size_t nv = NF * n;
+  auto load = [&](size_t v) {
+    fq12_t g;
+    g.h.c0 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 0));
+    g.h.c1 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 1));
+    g.h.c2 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 2));
+    return g;
+  };
+  fq12_t f = load(NF * i);
+  for (int k = 1; k < NF; ++k) f = fq12_mul(f, load(NF * i + k));
+  const bool one = fq12_is_one(final_exp_q(f));
   if (lead) verdict[i] = one ? 1 : 0;
 }
 

@@ -159,6 +159,9 @@ __device__ __forceinline__ fp2p_t fp2_sub2(const fp2p_t& a, const fp2p_t& b, con
 }
 __device__ __forceinline__ fp2p_t fp2_3m2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3m2(X.v, x.v)); }
 __device__ __forceinline__ fp2p_t fp2_3p2(const fp2p_t& X, const fp2p_t& x) { return pr_make(fp_3p2(X.v, x.v)); }
+__device__ __forceinline__ fp2p_t fp2_3pm2(const fp2p_t& X, const fp2p_t& x, bool minus) {
+  return pr_make(fp_3pm2(X.v, x.v, minus));
+}
 #if BLS_FP2_INLINE == 2
 // inlined bodies fenced by scheduling barriers: the scheduler cannot interleave
 // two products, so the live set stays one product's temporaries + the caller's state

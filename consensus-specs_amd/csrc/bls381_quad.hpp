@@ -160,4 +160,274 @@ fq12_t miller_loop_quad(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool activ
   return fq12_conj(f);
 }
 
+// ------------------------------------------------ one Miller pair per quad --
+// The latency form of the Miller loop: one pair per quad, T held on both halves,
+// and the independent products of every step split over the halves:
+//   doubling (line_dbl)       11 products -> 6 steps
+//   addition (line_add)       15 products -> 8 steps
+//   f * line (sparse)         13 products -> 7 steps
+//   f^2                       12 products -> 6 steps (fq12_sqr)
+// so a doubling iteration is 19 product steps against 30 for the two-pair quad
+// loop above (and 36 for one pair on a lane pair).  Values computed on both
+// halves from the same inputs stay bit-identical, so T needs no exchange.
+
+// line_dbl with its products split: lo X^2 | hi Y^2, lo Z^2 | hi YZ, XY (both);
+// then lo XX(-3xp) | hi YZ(2yp), lo XY(YY - 9b'Z^2) | hi YY YZ, lo h^2 | hi (3b'Z^2)^2
+__device__ __forceinline__ void line_dbl_q1(g2_proj<fp2p_t>& T, const g1_line_pre& P, fp2p_t& c0, fp2p_t& c1,
+                                            fp2p_t& c2) {
+  const bool hi = qd_hi();
+  const fp2p_t s1 = fp2_sqr(qd_sel(hi, T.y, T.x));
+  const fp2p_t m1 = fp2_mul(T.z, qd_sel(hi, T.y, T.z));
+  const fp2p_t XY = fp2_mul(T.x, T.y);
+  const fp2p_t s1o = qd_swap(s1), m1o = qd_swap(m1);
+  const fp2p_t XX = qd_sel(hi, s1o, s1), YY = qd_sel(hi, s1, s1o);
+  const fp2p_t ZZ = qd_sel(hi, m1o, m1), YZ = qd_sel(hi, m1, m1o);
+  const fp2p_t b3 = fp2_mul_small(fp2_mul_small(fp2_mul_xi(ZZ), 3), 4);   // 3 b' Z^2
+  const fp2p_t b9 = fp2_mul_small(b3, 3);
+  c0 = fp2_sub(YY, b3);
+  const fp2p_t e = fp2_mul_fp(qd_sel(hi, YZ, XX), fp_sel(hi, P.y2, P.n3x));
+  const fp2p_t h = fp2_half(fp2_add(YY, b9));
+  const fp2p_t m2 = fp2_mul(qd_sel(hi, YY, XY), qd_sel(hi, YZ, fp2_sub(YY, b9)));
+  const fp2p_t s2 = fp2_sqr(qd_sel(hi, b3, h));
+  const fp2p_t eo = qd_swap(e), m2o = qd_swap(m2), s2o = qd_swap(s2);
+  c1 = qd_sel(hi, eo, e);
+  c2 = qd_sel(hi, e, eo);
+  T.x = fp2_half(qd_sel(hi, m2o, m2));
+  T.y = fp2_sub(qd_sel(hi, s2o, s2), fp2_mul_small(qd_sel(hi, s2, s2o), 3));
+  T.z = fp2_dbl(qd_sel(hi, m2, m2o));
+}
+
+// line_add with its products split (lo | hi per step)
+__device__ __forceinline__ void line_add_q1(g2_proj<fp2p_t>& T, const aff_t<fp2p_t>& Q, const g1_line_pre& P,
+                                            fp2p_t& c0, fp2p_t& c1, fp2p_t& c2) {
+  const bool hi = qd_hi();
+  auto both = [&](const fp2p_t& mine, fp2p_t& lo_v, fp2p_t& hi_v) {
+    const fp2p_t o = qd_swap(mine);
+    lo_v = qd_sel(hi, o, mine);
+    hi_v = qd_sel(hi, mine, o);
+  };
+  fp2p_t a, b;
+  both(fp2_mul(T.z, qd_sel(hi, Q.x, Q.y)), a, b);                        // yq Z | xq Z
+  const fp2p_t u = fp2_sub(a, T.y), v = fp2_sub(b, T.x);
+  both(fp2_mul(qd_sel(hi, v, u), qd_sel(hi, Q.y, Q.x)), a, b);           // u xq | v yq
+  c0 = fp2_sub(a, b);
+  both(fp2_mul_fp(qd_sel(hi, v, u), fp_sel(hi, P.y, P.nx)), c1, c2);     // -u xp | v yp
+  fp2p_t vv, uu;
+  both(fp2_sqr(qd_sel(hi, u, v)), vv, uu);
+  fp2p_t vvv, vvX;
+  both(fp2_mul(vv, qd_sel(hi, T.x, v)), vvv, vvX);
+  fp2p_t uuZ, vvvZ;
+  both(fp2_mul(T.z, qd_sel(hi, vvv, uu)), uuZ, vvvZ);
+  const fp2p_t A = fp2_sub2(uuZ, vvv, fp2_dbl(vvX));
+  fp2p_t vvvY, vA;
+  both(fp2_mul(qd_sel(hi, v, vvv), qd_sel(hi, A, T.y)), vvvY, vA);
+  T.y = fp2_sub(fp2_mul(u, fp2_sub(vvX, A)), vvvY);
+  T.x = vA;
+  T.z = vvvZ;
+}
+
+// f * (c0 + c1 v + c2 v w) with the 13 products split 7 | 6 (lo: a = f.c0, hi: b = f.c1):
+//   lo: aA (5 products of fp12_mul_by_line_inl), s2 d1, s2 c0
+//   hi: bB (3), s0 c0, s1 d1, (s0 + s1)(c0 + d1)     with s = a + b, d1 = c1 + c2
+__device__ __forceinline__ fq12_t fq12_mul_by_line_q1(const fq12_t& f, const fp2p_t& c0, const fp2p_t& c1,
+                                                      const fp2p_t& c2) {
+  const bool hi = qd_hi();
+  const fp6p_t& h = f.h;
+  fp6p_t s = fp6_add(h, qd_swap(h));
+  const fp2p_t d1 = fp2_add(c1, c2);
+  const fp2p_t p0 = fp2_mul(qd_sel(hi, h.c2, h.c0), qd_sel(hi, c2, c0));                    // a0c0 | b2c2
+  const fp2p_t p1 = fp2_mul(qd_sel(hi, h.c0, h.c1), qd_sel(hi, c2, c1));                    // a1c1 | b0c2
+  const fp2p_t p2 = fp2_mul(qd_sel(hi, h.c1, h.c2), qd_sel(hi, c2, c1));                    // a2c1 | b1c2
+  const fp2p_t p3 = fp2_mul(qd_sel(hi, s.c0, fp2_add_lazy(h.c0, h.c1)), qd_sel(hi, c0, fp2_add_lazy(c0, c1)));  // (a0+a1)(c0+c1) | s0c0
+  const fp2p_t p4 = fp2_mul(qd_sel(hi, s.c1, h.c2), qd_sel(hi, d1, c0));                    // a2c0 | s1d1
+  const fp2p_t p5 = fp2_mul(qd_sel(hi, fp2_add_lazy(s.c0, s.c1), s.c2),
+                            qd_sel(hi, fp2_add_lazy(c0, d1), d1));                          // s2d1 | (s0+s1)(c0+d1)
+  const fp2p_t p6 = fp2_mul(s.c2, c0);                                                      // s2c0 (lo)
+  // lo: aA;  hi: bB = (xi b2c2, b0c2, b1c2)
+  fp6p_t X;
+  X.c0 = qd_sel(hi, fp2_mul_xi(p0), fp2_add_mul_xi(p0, p2));
+  X.c1 = qd_sel(hi, p1, fp2_sub2(p3, p0, p1));
+  X.c2 = qd_sel(hi, p2, fp2_add(p1, p4));
+  const fp6p_t Y = qd_swap(X);                       // lo: bB, hi: aA
+  const fp2p_t q5 = qd_swap(p5), q6 = qd_swap(p6);    // hi: s2d1, s2c0 (lo's)
+  fq12_t r;
+  // lo: aA + v bB
+  const fp6p_t lo = fp6_add_mul_by_v(X, Y);
+  // hi: m - aA - bB,  m = (s0c0 + xi s2d1, (s0+s1)(c0+d1) - s0c0 - s1d1, s1d1 + s2c0)
+  fp6p_t m;
+  m.c0 = fp2_add_mul_xi(p3, q5);
+  m.c1 = fp2_sub2(p5, p3, p4);
+  m.c2 = fp2_add(p4, q6);
+  r.h = qd_sel(hi, fp6_sub2(m, Y, X), lo);
+  return r;
+}
+
+// Miller loop of one pair on a quad; returns conj(f) (x < 0).  degenerate as in miller_loop_n.
+__device__ __noinline__ fq12_t miller_loop_q1(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool& degenerate) {
+  g2_proj<fp2p_t> T;
+  T.x = Q.x; T.y = Q.y; T.z = e2_one<fp2p_t>();
+  fq12_t f = fq12_one();
+  bool first = true;
+  for (int i = 62; i >= 0; --i) {
+    fp2p_t c0, c1, c2;
+    line_dbl_q1(T, P, c0, c1, c2);
+    if (!first) f = fq12_sqr(f);
+    f = fq12_mul_by_line_q1(f, c0, c1, c2);
+    first = false;
+    if ((BLS_X_ABS >> i) & 1) {
+      line_add_q1(T, Q, P, c0, c1, c2);
+      f = fq12_mul_by_line_q1(f, c0, c1, c2);
+    }
+  }
+  degenerate = fp2_is_zero(T.z);   // T is the same on all four lanes
+  return fq12_conj(f);
+}
+
+// ------------------------------------------- final exponentiation on quads --
+// The latency form of final_exp (bls381_pairing.hpp): the same chain, with every
+// Fp12 step split over the two halves, for batches too small to fill the GPU
+// (single calls, verify_multiple batches, randomized sub-batches).
+
+// f^(q^p): lo holds the coefficients of w^0, w^2, w^4, hi those of w^1, w^3, w^5
+__device__ __forceinline__ fq12_t fq12_frob(const fq12_t& f, int p) {
+  const fp2_t* g = FROB_GAMMA_M[p - 1];
+  const bool hi = qd_hi();
+  const bool odd = (p & 1) != 0;
+  auto fr = [&](const fp2p_t& c, int j) -> fp2p_t {
+    const fp2p_t cc = odd ? fp2_conj(c) : c;
+    return fp2_mul(cc, qd_sel(hi, e2_k<fp2p_t>(g[2 * j + 1]), e2_k<fp2p_t>(g[2 * j])));
+  };
+  fq12_t r;
+  r.h.c0 = fr(f.h.c0, 0);
+  r.h.c1 = fr(f.h.c1, 1);
+  r.h.c2 = fr(f.h.c2, 2);
+  return r;
+}
+
+// 1/(a + b w) = (a - b w) / (a^2 - v b^2): lo squares a, hi b; the Fp6 inverse
+// runs on both halves
+__device__ __forceinline__ fq12_t fq12_inv(const fq12_t& f) {
+  const bool hi = qd_hi();
+  const fp6p_t p = fp6_mul_inl(f.h, f.h);
+  const fp6p_t o = qd_swap(p);
+  const fp6p_t t = fp6_sub(qd_sel(hi, o, p), fp6_mul_by_v(qd_sel(hi, p, o)));
+  const fp6p_t r = fp6_mul_inl(f.h, fp6_inv(t));
+  fq12_t out;
+  out.h = qd_sel(hi, fp6_neg(r), r);
+  return out;
+}
+
+__device__ __forceinline__ bool fq12_is_one(const fq12_t& f) {
+  const bool hi = qd_hi();
+  const bool a = fp2_eq(f.h.c0, qd_sel(hi, e2_zero<fp2p_t>(), e2_one<fp2p_t>()));
+  const bool b = fp2_is_zero(f.h.c1);
+  const bool c = fp2_is_zero(f.h.c2);
+  return qd_all(a & b & c);
+}
+
+// Karabina compressed squaring (cyc_csqr) on a quad.  lo holds (x, y) = (g4, g5)
+// and squares them (t0, t1, t2 of cyc_csqr), hi holds (g2, g3) (t3, t4, t5); each
+// half's outputs update the other half's pair, so one exchange per squaring:
+// three Fp2 squarings per lane instead of six.
+struct cq_t { fp2p_t x, y; };
+
+__device__ __forceinline__ cq_t cq_compress(const fq12_t& f) {
+  // g2 = b0 (hi c0), g3 = a2 (lo c2), g4 = a1 (lo c1), g5 = b2 (hi c2)
+  cq_t g;
+  g.x = qd_sel(qd_hi(), f.h.c0, f.h.c1);
+  g.y = qd_swap(f.h.c2);
+  return g;
+}
+
+__device__ __forceinline__ cq_t cq_sqr(const cq_t& g) {
+  const bool hi = qd_hi();
+  const fp2p_t s0 = fp2_sqr(g.x), s1 = fp2_sqr(g.y), s2 = fp2_sqr(fp2_add(g.x, g.y));
+  const fp2p_t D = fp2_sub2(s2, s0, s1);       // 2 x y
+  const fp2p_t S = fp2_add_mul_xi(s0, s1);     // x^2 + xi y^2
+  const fp2p_t U = qd_swap(qd_sel(hi, S, fp2_mul_xi(D)));   // lo <- S(hi), hi <- xi D(lo)
+  const fp2p_t V = qd_swap(qd_sel(hi, D, S));               // lo <- D(hi), hi <- S(lo)
+  cq_t r;
+  r.x = fp2_3pm2(U, g.x, !hi);   // lo: g4' = 3 (g2^2 + xi g3^2) - 2 g4;  hi: g2' = 6 xi g4 g5 + 2 g2
+  r.y = fp2_3pm2(V, g.y, hi);    // lo: g5' = 6 g2 g3 + 2 g5;             hi: g3' = 3 (g4^2 + xi g5^2) - 2 g3
+  return r;
+}
+
+// g2 of a compressed value, on all four lanes
+__device__ __forceinline__ fp2p_t cq_g2(const cq_t& g) { return qd_sel(qd_hi(), g.x, qd_swap(g.x)); }
+
+// cyc_decompress on a quad; inv = 1 / (4 g2) on all lanes
+__device__ __forceinline__ fq12_t cq_decompress(const cq_t& g, const fp2p_t& inv) {
+  const bool hi = qd_hi();
+  const fp2p_t xo = qd_swap(g.x), yo = qd_swap(g.y);
+  const fp2p_t G2 = qd_sel(hi, g.x, xo), G3 = qd_sel(hi, g.y, yo);
+  const fp2p_t G4 = qd_sel(hi, xo, g.x), G5 = qd_sel(hi, yo, g.y);
+  const fp2p_t sq = fp2_sqr(qd_sel(hi, G5, G4));             // lo: g4^2, hi: g5^2
+  const fp2p_t sqo = qd_swap(sq);
+  const fp2p_t num = fp2_sub2(fp2_add_mul_xi(fp2_mul_small(qd_sel(hi, sqo, sq), 3), qd_sel(hi, sq, sqo)), G3, G3);
+  const fp2p_t p1 = fp2_mul(qd_sel(hi, G3, num), qd_sel(hi, G4, inv));   // lo: b1, hi: g3 g4
+  const fp2p_t p2 = fp2_mul(qd_sel(hi, G2, p1), qd_sel(hi, G5, p1));     // lo: b1^2, hi: g2 g5
+  const fp2p_t p1o = qd_swap(p1), p2o = qd_swap(p2);
+  const fp2p_t u = fp2_sub(fp2_add(fp2_dbl(p2), p2o), fp2_mul_small(p1o, 3));   // lo: 2 b1^2 + g2 g5 - 3 g3 g4
+  fq12_t f;
+  f.h.c0 = qd_sel(hi, G2, fp2_add(fp2_mul_xi(u), e2_one<fp2p_t>()));   // b0 | a0
+  f.h.c1 = qd_sel(hi, p1o, G4);                                        // b1 | a1
+  f.h.c2 = qd_sel(hi, G5, G3);                                         // b2 | a2
+  return f;
+}
+
+// exact fallback (cyc_exp_x_gs): generic squarings, valid for every element
+__device__ __noinline__ fq12_t cyc_exp_x_gs_q(const fq12_t& f) {
+  fq12_t r = f;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fq12_sqr(r);
+    if (s < 5) r = fq12_mul(r, f);
+  }
+  return fq12_conj(r);
+}
+
+// f^x (cyc_exp_x): compressed squarings, six snapshots, one shared inversion
+__device__ __noinline__ fq12_t cyc_exp_x_q(const fq12_t& f) {
+  const bool hi = qd_hi();
+  cq_t snap[6];
+  cq_t g = cq_compress(f);
+  bool zero = false;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cq_sqr(g);
+    snap[s] = g;
+    zero = zero | fp2_is_zero(cq_g2(g));
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs_q(f);
+  fp2p_t pre[6];
+  pre[0] = fp2_mul_small(cq_g2(snap[0]), 4);
+  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(cq_g2(snap[s]), 4));
+  fp2p_t inv = fp2_inv(pre[5]);
+  fq12_t r;
+  for (int s = 5; s >= 0; --s) {
+    fp2p_t is = inv;
+    if (s) {
+      // lo: inv * pre[s-1] (this snapshot's 1/(4 g2)), hi: inv * 4 g2 (the next inv)
+      const fp2p_t p = fp2_mul(inv, qd_sel(hi, fp2_mul_small(cq_g2(snap[s]), 4), pre[s - 1]));
+      const fp2p_t po = qd_swap(p);
+      is = qd_sel(hi, po, p);
+      inv = qd_sel(hi, p, po);
+    }
+    const fq12_t x = cq_decompress(snap[s], is);
+    r = (s == 5) ? x : fq12_mul(r, x);
+  }
+  return fq12_conj(r);
+}
+
+// f^(3 (q^12 - 1)/r), the chain of final_exp
+__device__ inline fq12_t final_exp_q(const fq12_t& f) {
+  fq12_t t = fq12_mul(fq12_conj(f), fq12_inv(f));          // f^(q^6 - 1)
+  t = fq12_mul(fq12_frob(t, 2), t);                        // ^(q^2 + 1)
+  fq12_t a = fq12_mul(cyc_exp_x_q(t), fq12_conj(t));       // t^(x-1)
+  a = fq12_mul(cyc_exp_x_q(a), fq12_conj(a));              // t^((x-1)^2)
+  const fq12_t b = fq12_mul(cyc_exp_x_q(a), fq12_frob(a, 1));          // a^(x+q)
+  const fq12_t bx2 = cyc_exp_x_q(cyc_exp_x_q(b));
+  const fq12_t c = fq12_mul(fq12_mul(bx2, fq12_frob(b, 2)), fq12_conj(b));   // b^(x^2+q^2-1)
+  const fq12_t t3 = fq12_mul(fq12_sqr(t), t);
+  return fq12_mul(c, t3);
+}
+
 }  // namespace bls381

@@ -178,10 +178,40 @@ def test_batch_against_oracle_small(native):
     assert list(v) == exp
 
 
-def test_batch_full_size_roundtrip(native):
-    """2^12 signed items (sign -> verify round trip), 1/4 tampered: size-independent check."""
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+@pytest.mark.parametrize("n", [100, 12000, 20000])
+def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
+    """The golden and torsion bls_verify cases (infinite keys and signatures, bad encodings,
+    small-order components, a degenerate Miller loop) tiled to n items, so every Miller /
+    final-exponentiation layout sees them: n <= 8192 one quad per Miller pair + the 2-value
+    quad FE, n <= 16384 both pairs on one quad + the quad FE, above that lane pairs.  The
+    tiled verdicts equal the untiled batch's, which equal the fixtures' py_ecc column."""
+    _, gb = golden
+    cases = [(c, c["expected"]) for c in gb["verify"] if len(bytes.fromhex(c["message"])) == 32]
+    cases += [(c, c["expected_pyecc"]) for c in torsion["verify"]]
+    assert all(len(bytes.fromhex(c["message"])) == 32 for c, _ in cases)
+
+    def run(items):
+        return list(native.verify_batch(b"".join(bytes.fromhex(c["pubkey"]) for c in items),
+                                        b"".join(bytes.fromhex(c["message"]) for c in items),
+                                        b"".join(bytes.fromhex(c["signature"]) for c in items),
+                                        b"".join(int(c["domain"]).to_bytes(8, "big") for c in items)))
+    native.set_subgroup_policy(policy)
+    try:
+        base = run([c for c, _ in cases])
+        tiled = run([cases[i % len(cases)][0] for i in range(n)])
+    finally:
+        native.set_subgroup_policy("pyecc")
+    if policy == "pyecc":
+        assert base == [e for _, e in cases]
+    assert tiled == [base[i % len(cases)] for i in range(n)]
+
+
+@pytest.mark.parametrize("n", [4096, 12000, 20000])
+def test_batch_full_size_roundtrip(native, n):
+    """Signed items (sign -> verify round trip), 1/4 tampered, at sizes that run each Miller /
+    final-exponentiation layout: size-independent check."""
     from bls381_amd import bls
-    n = 4096
     rng = np.random.default_rng(7)
     # one key, many messages: signing cost stays small, verify work per item is full
     sk = 0x1234567890ABCDEF
@@ -279,6 +309,28 @@ def test_verify_multiple_batch_golden(native, golden):
         off.append(off[-1] + len(c["pubkeys"]))
     v = native.verify_multiple_batch(off, pks, msgs, 32, sigs, doms)
     assert list(v) == [c["expected"] for c in cases]
+
+
+@pytest.mark.parametrize("reps", [1, 700])
+def test_verify_multiple_batch_layouts_tiled(native, golden, torsion, reps):
+    """Golden + torsion verify_multiple cases repeated `reps` times in one batch: reps = 1 runs
+    one lane quad per Miller pair (k_miller_tasks_q1, <= 8192 pairs), reps = 700 two pairs
+    per quad (k_miller_quads).  Per-call verdicts == the fixtures' py_ecc column."""
+    _, gb = golden
+    cases = [(c, c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+    cases += [(c, c["expected_pyecc"]) for c in torsion["verify_multiple"]]
+    off, pks, msgs, sigs, doms, want = [0], [], [], [], [], []
+    for _ in range(reps):
+        for c, e in cases:
+            pks += [bytes.fromhex(p) for p in c["pubkeys"]]
+            msgs += [bytes.fromhex(m) for m in c["messages"]]
+            sigs.append(bytes.fromhex(c["signature"]))
+            doms.append(int(c["domain"]).to_bytes(8, "big"))
+            off.append(off[-1] + len(c["pubkeys"]))
+            want.append(e)
+    assert all(len(m) == 32 for m in msgs)
+    v = native.verify_multiple_batch(off, b"".join(pks), b"".join(msgs), 32, b"".join(sigs), b"".join(doms))
+    assert list(v) == want
 
 
 def _committee_calls(rng, n_calls, max_keys, sks):
