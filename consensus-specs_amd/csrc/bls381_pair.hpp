@@ -313,15 +313,24 @@ __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* ms
   // Search with the cheap Legendre test only, then take one square root after
   // the loop: inside the loop the root's exponentiations would run (under a
   // partial exec mask) in every trial in which any lane of the wave succeeds.
-  // rhs is a square in Fp2 iff its norm is a square in Fp (both lanes, same norm).
+  // rhs is a square in Fp2 iff its norm is a square in Fp.  Each round tests two
+  // consecutive candidates, one Legendre symbol per lane (lane 0: x, lane 1: x + 1),
+  // and keeps the first square in candidate order: the spec's x, in half the
+  // sequential Legendre evaluations.
   int trials = 0;
   fp2p_t rhs;
   while (true) {
-    ++trials;
-    rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
-    const fp_t t = fp_sqr(rhs.v);
-    if (fp_legendre(fp_add(t, pr_dpp<DPP_SWAP>(t))) >= 0) break;
-    x.v = fp_add(x.v, inc);
+    trials += 2;
+    const fp2p_t x1 = pr_make(fp_add(x.v, inc));
+    const fp2p_t r0 = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
+    const fp2p_t r1 = fp2_add(fp2_mul(fp2_sqr(x1), x1), e2_k<fp2p_t>(G2_B_M));
+    const fp_t t0 = fp_sqr(r0.v), t1 = fp_sqr(r1.v);
+    const fp_t n0 = fp_add(t0, pr_dpp<DPP_SWAP>(t0)), n1 = fp_add(t1, pr_dpp<DPP_SWAP>(t1));
+    const uint32_t sq = fp_legendre(odd ? n1 : n0) >= 0 ? 1u : 0u;
+    const bool ok0 = pr_dpp<DPP_EVEN>(sq) != 0, ok1 = pr_dpp<DPP_ODD>(sq) != 0;
+    if (ok0) { rhs = r0; break; }
+    if (ok1) { x = x1; rhs = r1; break; }
+    x.v = fp_add(x1.v, inc);
   }
   fp2p_t y;
   fp2_sqrt(y, rhs);   // succeeds: rhs is a square
