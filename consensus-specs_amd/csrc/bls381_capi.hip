@@ -50,7 +50,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   // side stream + fork/join events: independent stages of one batch run concurrently
   hipStream_t side = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
   std::mutex fork_mu;
   void* ws = nullptr;
   size_t ws_cap = 0;
@@ -108,7 +108,8 @@ Ctx* get_ctx(int* rc) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
       delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
     }
     g_ctx[dev] = c;
@@ -546,8 +547,8 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, si
   }
   pl.nquads = pl.quad_pair.size() / 2;
   if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
-  if (2 * pl.nquads <= BLS_VM_TASK_MAX) {
-    pl.tasks = true;
+  pl.tasks = 2 * pl.nquads <= BLS_VM_TASK_MAX;
+  if (pl.tasks) {
     std::vector<uint32_t> toff(pl.call_quad_off.size());
     for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
     pl.task_passes = plan_products(toff);
@@ -2088,7 +2089,7 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
 namespace {
 
 size_t rb_ws_size(size_t n, size_t B) {
-  const size_t nb = (n + B - 1) / B, nslots = nb * (B / 2 + 1);
+  const size_t nb = (n + B - 1) / B, nslots = nb * (B + 1);
   size_t s = verify_ws_size(n) + 4 * 65536;
   s += align256(2 * FPW * n) + 3 * align256(n) + align256(6 * FPW * n) + align256(n);   // R1, statuses, R2, zeros
   const size_t ch = nb + n / CHUNK_L1 + 1;                                              // R2 sums per sub-batch
@@ -2103,7 +2104,7 @@ size_t rb_ws_size(size_t n, size_t B) {
 int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
                           const uint8_t* doms, const uint8_t* seed32, size_t B, uint8_t* d_verdicts, void* ws,
                           size_t ws_cap, hipStream_t s, uint64_t* stats) {
-  const size_t nb = (n + B - 1) / B, half = B / 2, nslots = nb * (half + 1);
+  const size_t nb = (n + B - 1) / B, nslots = nb * (B + 1);
   Bump b(ws, ws_cap);
   VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n)), n);
   uint32_t* r1 = b.take<uint32_t>(2 * FP_LIMBS * n);
@@ -2117,46 +2118,52 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   auto seed = std::make_shared<std::vector<uint8_t>>(seed32, seed32 + 32);
   HIPC(hipMemcpyAsync(d_seed, seed->data(), 32, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(zeros, 0, n, s));
-  {
-    std::lock_guard<std::mutex> lk(c->fork_mu);
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    LAUNCH("decode_g1", c->side, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
-    // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-    LAUNCH("decode_g2", c->side, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
-    HIPC(hipEventRecord(c->ev_join, c->side));
-    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st);
-    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
-  }
-  LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
-         (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
-  LAUNCH("rb_scale_g2", s, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
-         (const uint8_t*)w.sig_st, (const uint8_t*)cls, r2);
-  // per sub-batch sum of [r_i] sig_i
+  // Miller values: B item slots per sub-batch + its signature-sum slot
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nslots);
+  uint8_t* fst = b.take<uint8_t>(nslots);
+  // per sub-batch sum of [r_i] sig_i (planned here; runs on the side stream)
   std::vector<uint32_t> off(nb + 1);
   for (size_t k = 0; k <= nb; ++k) off[k] = (uint32_t)std::min(n, k * B);
   auto plan = std::make_shared<AggPlan>(plan_agg(nb, off.data()));
-  const uint32_t* sjac;
-  const uint8_t* sbad;
-  size_t used = 0;
-  uint8_t* sub = b.take<uint8_t>(0);
-  int rc = run_agg<fp2p_t>(*plan, nb, nullptr, sub, s, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n);
-  if (rc) return rc;
-  b.off += used;
   uint32_t* s_aff = b.take<uint32_t>(4 * FP_LIMBS * nb);
   uint8_t* s_st = b.take<uint8_t>(nb);
-  LAUNCH("agg_g2_affine", s, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
-  // Miller values: B/2 two-pair slots per sub-batch + its signature-sum slot
-  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nslots);
-  uint8_t* fst = b.take<uint8_t>(nslots);
-  const size_t nitems = nb * half;
-  LAUNCH("rb_miller_items", s, dim3(grid_for(2 * nitems)), blk, k_rb_miller_items, n, half, nitems,
-         (const uint32_t*)w.h_aff, (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st,
-         (const uint8_t*)cls, nslots, f, fst);
-  LAUNCH("rb_miller_sig", s, dim3(grid_for(2 * nb)), blk, k_rb_miller_sig, nb, half, (const uint32_t*)s_aff,
-         (const uint8_t*)s_st, nslots, f, fst);
+  {
+    // side stream: decodes, then the whole signature branch ([r_i] sig_i, the sub-batch sums
+    // and their Miller loops on lane quads); main stream: hash_to_G2, [r_i] pk_i and the
+    // per-item Miller loops.  The branches join before the segmented products.
+    std::lock_guard<std::mutex> lk(c->fork_mu);
+    hipStream_t side = c->side;
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(side, c->ev_fork, 0));
+    LAUNCH("decode_g1", side, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
+    LAUNCH("decode_g2", side, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
+    HIPC(hipEventRecord(c->ev_join, side));
+    LAUNCH("rb_scale_g2", side, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
+           (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
+    const uint32_t* sjac;
+    const uint8_t* sbad;
+    size_t used = 0;
+    uint8_t* sub = b.take<uint8_t>(0);
+    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, side, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
+      return e;
+    b.off += used;
+    LAUNCH("agg_g2_affine", side, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
+    LAUNCH("rb_miller_sig", side, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, B, (const uint32_t*)s_aff,
+           (const uint8_t*)s_st, nslots, f, fst);
+    HIPC(hipEventRecord(c->ev_join2, side));
+    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st);
+    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
+           (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
+    LAUNCH("rb_miller_items", s, dim3(grid_for(2 * nb * B)), blk, k_rb_miller_items, n, B, nb * B,
+           (const uint32_t*)w.h_aff, (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st,
+           (const uint8_t*)cls, nslots, f, fst);
+    HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
+  }
+  int rc = 0;
   std::vector<uint32_t> seg(nb + 1);
-  for (size_t k = 0; k <= nb; ++k) seg[k] = (uint32_t)(k * (half + 1));
+  for (size_t k = 0; k <= nb; ++k) seg[k] = (uint32_t)(k * (B + 1));
   auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products(seg));
   size_t n_in = nslots;
   for (const auto& chunks : *passes) {

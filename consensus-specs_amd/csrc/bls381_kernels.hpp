@@ -377,16 +377,18 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t
   r1_st[i] = st;
 }
 
-// per item, one lane pair: R2 = [r_i] sig_i (Jacobian SoA; infinity when the item is not batched)
+// per item, one lane pair: R2 = [r_i] sig_i (Jacobian SoA; infinity when the item is not
+// batched: a bad pubkey, or a signature that is not a finite point of G2 -- the class
+// k_rb_scale_g1 assigns, recomputed from the statuses so this branch needs no cls)
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g2(size_t n, const uint8_t* __restrict__ seed32,
                                                        const uint32_t* __restrict__ sig_aff,
                                                        const uint8_t* __restrict__ sig_st,
-                                                       const uint8_t* __restrict__ cls,
+                                                       const uint8_t* __restrict__ pk_st,
                                                        uint32_t* __restrict__ r2_jac) {
   const size_t i = item_index<2>();
   if (i >= n) return;
   jac_t<fp2p_t> r = jac_infinity<fp2p_t>();
-  if (cls[i] == RB_BATCH && sig_st[i] == ST_OK) r = jac_mul_u64(soa_ld_g2(sig_aff, n, i), rb_scalar(seed32, i));
+  if (pk_st[i] != ST_BAD && sig_st[i] == ST_OK) r = jac_mul_u64(soa_ld_g2(sig_aff, n, i), rb_scalar(seed32, i));
   soa_jac<fp2p_t>::st(r2_jac, n, i, r);
 }
 
@@ -404,57 +406,57 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g2_affine(size
   if (lead) st[g] = ST_OK;
 }
 
-// Miller values of one sub-batch layout: sub-batch b owns slots [b (B/2 + 1), (b + 1)(B/2 + 1)):
-// B/2 item slots (lane pair j: items 2j, 2j + 1, pairs (H, R1)) and the signature-sum slot.
-// Item slots past the last item hold 1.
-__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_items(size_t n, size_t half_b, size_t nslots_items,
+// Miller values of one sub-batch layout: sub-batch b owns slots [b (B + 1), (b + 1)(B + 1)):
+// B item slots (item bB + k at slot b (B + 1) + k, its pair (H, R1), one item per lane
+// pair: 2n lanes, two waves per SIMD at 2^16 items) and the signature-sum slot.  Item
+// slots past the last item, and items outside the batch, hold 1.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_items(size_t n, size_t B, size_t nitem_slots,
                                                            const uint32_t* __restrict__ h_aff,
                                                            const uint8_t* __restrict__ h_st,
                                                            const uint32_t* __restrict__ r1_aff,
                                                            const uint8_t* __restrict__ r1_st,
                                                            const uint8_t* __restrict__ cls, size_t nslots,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t j = item_index<2>();
-  if (j >= nslots_items) return;
-  const size_t slot = (j / half_b) * (half_b + 1) + j % half_b;
-  aff_t<fp2p_t> Q[2];
-  g1_line_pre P[2];
-  int np = 0;
-  for (int t = 0; t < 2; ++t) {
-    const size_t i = 2 * j + t;
-    if (i < n && cls[i] == RB_BATCH && r1_st[i] == ST_OK && h_st[i] == ST_OK) {
-      Q[np] = soa_ld_g2(h_aff, n, i);
-      P[np] = g1_prepare(soa_ld_g1(r1_aff, n, i));
-      ++np;
-    }
-  }
-  fp12p_t f;
+  const size_t i = item_index<2>();
+  if (i >= nitem_slots) return;
+  const size_t slot = (i / B) * (B + 1) + i % B;
+  fp12p_t f = fp12_one<fp2p_t>();
   bool degen = false;
-  if (np == 2) f = miller_loop_n<2>(Q, P, degen);
-  else if (np == 1) f = miller_loop_n<1>(Q, P, degen);
-  else f = fp12_one<fp2p_t>();
+  if (i < n && cls[i] == RB_BATCH && r1_st[i] == ST_OK && h_st[i] == ST_OK) {
+    const aff_t<fp2p_t> Q = soa_ld_g2(h_aff, n, i);
+    const g1_line_pre P = g1_prepare(soa_ld_g1(r1_aff, n, i));
+    f = miller_loop_n<1>(&Q, &P, degen);
+  }
   soa_st12(f_out, nslots, slot, f);
   if (!pr_odd()) st_out[slot] = degen ? ST_BAD : ST_OK;
 }
 
-__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t half_b,
+// the signature-sum slot of every sub-batch: (sum_i [r_i] sig_i, -[c] g1), one lane quad
+// per sub-batch (miller_loop_q1, the latency form: nb is small and this branch runs
+// beside the per-item work)
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t B,
                                                          const uint32_t* __restrict__ s_aff,
                                                          const uint8_t* __restrict__ s_st, size_t nslots,
                                                          uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t b = item_index<2>();
+  const size_t b = item_index<4>();
   if (b >= nb) return;
-  const size_t slot = b * (half_b + 1) + half_b;
-  fp12p_t f = fp12_one<fp2p_t>();
+  const size_t slot = b * (B + 1) + B;
+  const int p = pr_odd() ? 1 : 0;
+  fq12_t f = fq12_one();
   bool degen = false;
   const uint8_t st = s_st[b];
   if (st == ST_OK) {
-    aff_t<fp2p_t> Q = soa_ld_g2(s_aff, nb, b);
+    aff_t<fp2p_t> Q;
+    Q.x = pr_make(soa_ld(s_aff, 2 * nb, 2 * b + p, 0));
+    Q.y = pr_make(soa_ld(s_aff, 2 * nb, 2 * b + p, 1));
     aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
-    g1_line_pre P = g1_prepare(ng);
-    f = miller_loop_n<1>(&Q, &P, degen);
+    f = miller_loop_q1(Q, g1_prepare(ng), degen);
   }
-  soa_st12(f_out, nslots, slot, f);
-  if (!pr_odd()) st_out[slot] = (st == ST_BAD || degen) ? ST_BAD : ST_OK;
+  const int c0 = qd_hi() ? 3 : 0;
+  soa_st(f_out, 2 * nslots, 2 * slot + p, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * nslots, 2 * slot + p, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * nslots, 2 * slot + p, c0 + 2, f.h.c2.v);
+  if ((threadIdx.x & 3u) == 0) st_out[slot] = (st == ST_BAD || degen) ? ST_BAD : ST_OK;
 }
 
 // ---------------------------------------------------- aggregation kernels --
