@@ -116,6 +116,38 @@ __global__ void __launch_bounds__(128, 2) k_fp12mul(size_t nl, int reps, const u
   for (int i = 0; i < reps; ++i) f = fp12_mul(f, g);
   st12(out, nl, lane, f);
 }
+__global__ void __launch_bounds__(128, 2) k_fp12mul_inl(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  fp12p f = ld12(in, nl, lane), g = ld12(in + 6 * 14 * nl, nl, lane);
+  for (int i = 0; i < reps; ++i) f = fp12_mul_inl(f, g);
+  st12(out, nl, lane, f);
+}
+__global__ void __launch_bounds__(128, 2) k_decomp(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  cyc_bc<fp2p_t> g;
+  g.g2.v = ld(in, nl, lane, 0); g.g3.v = ld(in, nl, lane, 1); g.g4.v = ld(in, nl, lane, 2); g.g5.v = ld(in, nl, lane, 3);
+  fp2p_t inv = pr_make(ld(in, nl, lane, 4));
+  fp12p f = fp12_one<fp2p_t>();
+  for (int i = 0; i < reps; ++i) {
+    const fp12p x = cyc_decompress(g, inv);
+    g.g2 = x.c0.c0; inv = x.c1.c1;
+  }
+  st(out, nl, lane, 0, g.g2.v); st(out, nl, lane, 1, inv.v);
+}
+__global__ void __launch_bounds__(128, 2) k_ml1(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  KHEAD
+  aff_t<fp2p_t> Q;
+  Q.x.v = ld(in, nl, lane, 0); Q.y.v = ld(in, nl, lane, 1);
+  aff_t<fp_t> p; p.x = ld(in, nl, lane, 2); p.y = ld(in, nl, lane, 3);
+  const g1_line_pre P = g1_prepare(p);
+  fp12p f = fp12_one<fp2p_t>();
+  bool degen = false;
+  for (int i = 0; i < reps; ++i) {
+    const fp12p g = miller_loop_n<1>(&Q, &P, degen);
+    f.c0.c0 = fp2_add(f.c0.c0, g.c0.c0);
+  }
+  st12(out, nl, lane, f);
+}
 __global__ void __launch_bounds__(128, 2) k_cycexp(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
   KHEAD
   fp12p f = ld12(in, nl, lane);
@@ -198,6 +230,9 @@ int main(int argc, char** argv) {
       {"fp2_sqr (pair)", k_fp2sqr, 256, "op"},
       {"fp2_add_mul_xi (pair)", k_fp2add, 1024, "op"},
       {"fp_inv (xgcd)", k_inv, 8, "op"},
+      {"fp12_mul_inl (pair)", k_fp12mul_inl, 16, "op"},
+      {"cyc_decompress (pair)", k_decomp, 16, "op"},
+      {"miller_loop_n<1> (pair)", k_ml1, 1, "op"},
       {"fp2_inv (pair)", k_fp2inv, 8, "op"},
       {"cyc_csqr (pair)", k_csqr, 315, "op"},
       {"fp12_mul (pair)", k_fp12mul, 16, "op"},
