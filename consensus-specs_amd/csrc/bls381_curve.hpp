@@ -148,6 +148,23 @@ BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
   return r;
 }
 
+// [k0] a + [k1] s for 32-bit k0, k1 (Shamir's trick: one doubling chain, mixed additions);
+// with s = endo(a) for an endomorphism acting as [mu] this is [k0 + mu k1] a at half the
+// doublings of a 64-bit multiplication (the randomized-batch weights)
+template <class F>
+BLS_NOINLINE jac_t<F> jac_mul_2x32(const aff_t<F>& a, const aff_t<F>& s, uint32_t k0, uint32_t k1) {
+  jac_t<F> r = jac_infinity<F>();
+  const uint32_t any = k0 | k1;
+  int top = 31;
+  while (top > 0 && !((any >> top) & 1u)) --top;
+  for (int i = top; i >= 0; --i) {
+    if (i != top) r = jac_dbl(r);
+    if ((k0 >> i) & 1u) r = jac_add_aff(r, a);
+    if ((k1 >> i) & 1u) r = jac_add_aff(r, s);
+  }
+  return r;
+}
+
 // [k] p for a 64-bit scalar, Jacobian base
 template <class F>
 BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {

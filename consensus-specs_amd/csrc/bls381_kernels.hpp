@@ -343,15 +343,24 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
 // are verified one by one.
 enum : uint8_t { RB_BAD = 0, RB_BATCH = 1, RB_SINGLE = 2 };
 
-// r_i = the first 8 bytes of SHA-256(seed || i), i as 8 little-endian bytes; never 0
-__device__ __forceinline__ uint64_t rb_scalar(const uint8_t* seed32, uint64_t i) {
+// The weight of item i is r_i = k0 + mu k1 (mod r) with mu = -x^2 and (k1, k0) the first
+// 8 bytes of SHA-256(seed || i), i as 8 little-endian bytes (never both 0).  The 2^64
+// pairs give 2^64 distinct weights (|k0 - k0'| < 2^32 < x^2), the small-exponent test's
+// error bound.  mu acts through cheap endomorphisms, so [r_i] P is a joint 32-bit
+// multiplication (jac_mul_2x32): on G1 sigma(x, y) = (beta x, y) = [-x^2] P (a torsion
+// component of a py_ecc-policy pubkey is multiplied differently, but the reduced pairing
+// is trivial on it, as in the per-item path); on G2 -psi^2(Q) = [-x^2] Q (batched
+// signatures are in G2).
+struct rb_weight { uint32_t k0, k1; };
+__device__ __forceinline__ rb_weight rb_scalar(const uint8_t* seed32, uint64_t i) {
   uint8_t buf[40];
   for (int k = 0; k < 32; ++k) buf[k] = seed32[k];
   for (int k = 0; k < 8; ++k) buf[32 + k] = (uint8_t)(i >> (8 * k));
   uint32_t d[8];
   sha256(d, buf, 40);
-  const uint64_t r = ((uint64_t)d[0] << 32) | d[1];
-  return r ? r : 1;
+  rb_weight w{d[1], d[0]};
+  if ((w.k0 | w.k1) == 0) w.k0 = 1;
+  return w;
 }
 
 // per item, one lane: its class, and R1 = [r_i] pk_i affine (status OK / INF)
@@ -368,8 +377,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t
   cls[i] = c;
   uint8_t st = ST_INF;
   if (c == RB_BATCH && ps == ST_OK) {
+    const aff_t<fp_t> p = soa_ld_g1(pk_aff, n, i);
+    aff_t<fp_t> sp;                       // sigma(p) = [-x^2] p
+    sp.x = fp_mul(G1_BETA_M, p.x);
+    sp.y = p.y;
+    const rb_weight w = rb_scalar(seed32, i);
     aff_t<fp_t> a;
-    if (jac_to_aff(a, jac_mul_u64(soa_ld_g1(pk_aff, n, i), rb_scalar(seed32, i)))) {
+    if (jac_to_aff(a, jac_mul_2x32(p, sp, w.k0, w.k1))) {
       soa_st_g1(r1_aff, n, i, a);
       st = ST_OK;
     }
@@ -388,7 +402,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g2(size_t
   const size_t i = item_index<2>();
   if (i >= n) return;
   jac_t<fp2p_t> r = jac_infinity<fp2p_t>();
-  if (pk_st[i] != ST_BAD && sig_st[i] == ST_OK) r = jac_mul_u64(soa_ld_g2(sig_aff, n, i), rb_scalar(seed32, i));
+  if (pk_st[i] != ST_BAD && sig_st[i] == ST_OK) {
+    const aff_t<fp2p_t> q = soa_ld_g2(sig_aff, n, i);
+    aff_t<fp2p_t> sq = g2_psi(g2_psi(q));   // -psi^2(q) = [-x^2] q
+    sq.y = fp2_neg(sq.y);
+    const rb_weight w = rb_scalar(seed32, i);
+    r = jac_mul_2x32(q, sq, w.k0, w.k1);
+  }
   soa_jac<fp2p_t>::st(r2_jac, n, i, r);
 }
 
