@@ -247,10 +247,36 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
         step()
     torch.cuda.synchronize()
     t = _max_time(time.perf_counter() - t0, world, dist, dev)
+    # the same epoch as one grouped call (bls381_verify_multiple_grouped_device): the committee
+    # sums run beside hash_to_G2 instead of before it
+    call_groups = np.arange(0, 2 * nc + 1, 2, dtype=np.uint32)
+    gws = torch.empty(L.bls381_verify_multiple_grouped_workspace_size(nc, 2 * nc, nc * cs, 32), dtype=torch.uint8,
+                      device=dev)
+    d_ver2 = torch.zeros(nc, dtype=torch.uint8, device=dev)
+
+    def fused():
+        native.check(L.bls381_verify_multiple_grouped_device(
+            nc, call_groups.ctypes.data_as(ctypes.c_void_p), 2 * nc, offsets.ctypes.data_as(ctypes.c_void_p), msgs,
+            32, d_cpks.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(), d_ver2.data_ptr(), gws.data_ptr(),
+            ctypes.c_void_p(stream.cuda_stream)))
+
+    fused()
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ver2.cpu().numpy().astype(bool), expected), "C3 grouped verdict mismatch"
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        fused()
+    torch.cuda.synchronize()
+    tf = _max_time(time.perf_counter() - t1, world, dist, dev)
     return {"workload": "C3: %d committees x %d per GPU: 2 x bls_aggregate_pubkeys + bls_verify_multiple([agg, inf], "
                         "[m0, m1], sig, 2) each, 1/16 wrong message; device-resident (aggregates never leave HBM)"
                         % (nc, cs),
-            "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world}
+            "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world,
+            "grouped": {"api": "bls381_verify_multiple_grouped_device (aggregation fused beside hash_to_G2)",
+                        "attestations_per_s": nc * steps * world / tf, "ms_per_epoch_step": 1e3 * tf / steps}}
 
 
 def bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8):

@@ -61,6 +61,10 @@ _SIGS = {
                                                                       ctypes.c_size_t]),
     "bls381_verify_multiple_batch_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _u8p,
                                                            _u8p, _u8p, _u8p, _u8p]),
+    "bls381_verify_multiple_grouped_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t, ctypes.c_size_t,
+                                                                        ctypes.c_size_t, ctypes.c_size_t]),
+    "bls381_verify_multiple_grouped_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, _u8p,
+                                                             ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p, _u8p]),
     "bls381_miller_partial": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, ctypes.c_int,
                                              _u8p, _u8p]),
     "bls381_final_verify": (ctypes.c_int, [ctypes.c_size_t, _u8p]),

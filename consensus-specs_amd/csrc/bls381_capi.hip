@@ -49,7 +49,7 @@ struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   // side stream + fork/join events: independent stages of one batch run concurrently
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr, side2 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
   std::mutex fork_mu;
   void* ws = nullptr;
@@ -107,6 +107,7 @@ Ctx* get_ctx(int* rc) {
     c->device = dev;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
@@ -557,6 +558,75 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, si
   return pl;
 }
 
+// Host plan from caller-given groups (bls381_verify_multiple_grouped_device): the same
+// VmPlan as plan_vm, with key_idx the caller's key order; groups of one call with equal
+// messages are merged (first-occurrence order), empty groups dropped.
+VmPlan plan_vm_grouped(size_t n_calls, const uint32_t* call_group_off, const uint32_t* group_key_off,
+                       const uint8_t* msgs, size_t mlen) {
+  VmPlan pl;
+  pl.n_calls = n_calls;
+  const size_t ng_all = call_group_off[n_calls];
+  pl.n_keys = group_key_off[ng_all];
+  pl.group_off.push_back(0);
+  pl.call_quad_off.push_back(0);
+  pl.key_idx.reserve(pl.n_keys);
+  size_t maxc = 0;
+  for (size_t c = 0; c < n_calls; ++c) maxc = std::max<size_t>(maxc, call_group_off[c + 1] - call_group_off[c]);
+  size_t cap = 16;
+  while (cap < 2 * maxc) cap <<= 1;
+  std::vector<uint32_t> slot(cap), stamp(cap, 0), first, merged;
+  std::vector<std::vector<uint32_t>> extra;   // later groups merged into a distinct message (rare)
+  std::vector<int32_t> pairs;
+  auto same = [&](uint32_t a, uint32_t b) { return mlen == 0 || std::memcmp(msgs + mlen * a, msgs + mlen * b, mlen) == 0; };
+  for (size_t c = 0; c < n_calls; ++c) {
+    const uint32_t gen = (uint32_t)c + 1;
+    first.clear();
+    extra.clear();
+    for (uint32_t g = call_group_off[c]; g < call_group_off[c + 1]; ++g) {
+      if (group_key_off[g + 1] == group_key_off[g]) continue;   // the empty aggregate: pairing 1
+      size_t h = mlen ? (size_t)msg_hash(msgs + mlen * (size_t)g, mlen) & (cap - 1) : 0;
+      while (true) {
+        if (stamp[h] != gen) {
+          stamp[h] = gen;
+          slot[h] = (uint32_t)first.size();
+          first.push_back(g);
+          extra.emplace_back();
+          break;
+        }
+        if (same(first[slot[h]], g)) { extra[slot[h]].push_back(g); break; }
+        h = (h + 1) & (cap - 1);
+      }
+    }
+    pairs.clear();
+    for (size_t d = 0; d < first.size(); ++d) {
+      for (uint32_t k = group_key_off[first[d]]; k < group_key_off[first[d] + 1]; ++k) pl.key_idx.push_back(k);
+      for (uint32_t g : extra[d])
+        for (uint32_t k = group_key_off[g]; k < group_key_off[g + 1]; ++k) pl.key_idx.push_back(k);
+      pl.group_off.push_back((uint32_t)pl.key_idx.size());
+      pl.group_msg.insert(pl.group_msg.end(), msgs + mlen * first[d], msgs + mlen * (first[d] + 1));
+      pl.group_call.push_back((uint32_t)c);
+      pairs.push_back((int32_t)pl.G);
+      ++pl.G;
+    }
+    pairs.push_back(-(int32_t)c - 1);   // the signature pair (an infinite signature is idle on the device)
+    for (size_t k = 0; k < pairs.size(); k += 2) {
+      pl.quad_pair.push_back(pairs[k]);
+      pl.quad_pair.push_back(k + 1 < pairs.size() ? pairs[k + 1] : PAIR_NONE);
+    }
+    pl.call_quad_off.push_back((uint32_t)(pl.quad_pair.size() / 2));
+  }
+  pl.nquads = pl.quad_pair.size() / 2;
+  if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
+  pl.tasks = 2 * pl.nquads <= BLS_VM_TASK_MAX;
+  if (pl.tasks) {
+    std::vector<uint32_t> toff(pl.call_quad_off.size());
+    for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
+    pl.task_passes = plan_products(toff);
+  }
+  if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
+  return pl;
+}
+
 // Each lane quad runs (up to) two pairs of one call, one per half (bls381_quad.hpp).
 // A half's pair is idle for PAIR_NONE or an infinite operand (py_ecc: pairing 1);
 // any undecodable / bad operand makes the quad BAD; so does a degenerate loop.
@@ -740,9 +810,14 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
       b.off += used;
       LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
     }
-    LAUNCH("decode_g2", side, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, d_sigs, sig_aff, sig_st,
-           chk);
     HIPC(hipEventRecord(c->ev_join, side));
+    // the signature decodes on a second side stream: for an epoch of attestations the group
+    // sums and the decodes are each about as long as the hash, so in sequence they would
+    // outlast it
+    HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
+    LAUNCH("decode_g2", c->side2, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, d_sigs, sig_aff,
+           sig_st, chk);
+    HIPC(hipEventRecord(c->ev_join2, c->side2));
     if (G > 0) {
       LAUNCH("gather_domains", s, dim3(grid_for(8 * G)), dim3(KBLOCK), k_gather_rows, G, (const uint32_t*)d_gcall,
              d_doms, 8u, d_gdom);
@@ -750,6 +825,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
              (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st);
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
   }
   const size_t nf = pl.tasks ? 2 * nq : nq;
   uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nf);
@@ -851,9 +927,12 @@ void bls381_shutdown(void) {
     if (c->ws) (void)hipFree(c->ws);
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamSynchronize(c->side);
+    (void)hipStreamSynchronize(c->side2);
     (void)hipStreamDestroy(c->side);
+    (void)hipStreamDestroy(c->side2);
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
+    (void)hipEventDestroy(c->ev_join2);
     delete c;
   }
   g_ctx.clear();
@@ -1036,6 +1115,42 @@ int bls381_verify_multiple_batch_device(size_t n_calls, const uint32_t* h_call_o
   if ((rc = run_vm_batch(c, *pl, msg_len, d_pks, d_sigs, d_dom8s, b, s, &f, &st))) return rc;
   LAUNCH_FE(s, n_calls, f, st, d_verdicts);
   return keep_until_done(c, s, pl);   // the plan's arrays are async copy sources
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
+size_t bls381_verify_multiple_grouped_workspace_size(size_t n_calls, size_t n_groups, size_t n_pks, size_t msg_len) {
+  return vm_ws_bound_sizes(n_calls, std::max(n_pks, n_groups), msg_len) + align256(n_calls) + 4096;
+}
+
+int bls381_verify_multiple_grouped_device(size_t n_calls, const uint32_t* h_call_group_off, size_t n_groups,
+                                          const uint32_t* h_group_key_off, const uint8_t* h_group_msgs,
+                                          size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                          const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                          void* stream) try {
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  if (n_calls == 0) return 0;
+  if (!h_call_group_off || !h_group_key_off || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace ||
+      msg_len > BLS381_MSG_MAX)
+    return BLS381_EARG;
+  if (h_call_group_off[0] != 0 || h_call_group_off[n_calls] != n_groups || h_group_key_off[0] != 0) return BLS381_EARG;
+  for (size_t k = 0; k < n_calls; ++k)
+    if (h_call_group_off[k + 1] < h_call_group_off[k]) return BLS381_EARG;
+  for (size_t g = 0; g < n_groups; ++g)
+    if (h_group_key_off[g + 1] < h_group_key_off[g]) return BLS381_EARG;
+  const size_t nk = h_group_key_off[n_groups];
+  if ((nk && !d_pks) || (n_groups && msg_len && !h_group_msgs)) return BLS381_EARG;
+  auto pl = std::make_shared<VmPlan>(plan_vm_grouped(n_calls, h_call_group_off, h_group_key_off, h_group_msgs, msg_len));
+  hipStream_t s = (hipStream_t)stream;
+  Bump b(d_workspace, bls381_verify_multiple_grouped_workspace_size(n_calls, n_groups, nk, msg_len));
+  uint32_t* f;
+  uint8_t* st;
+  if ((rc = run_vm_batch(c, *pl, msg_len, d_pks, d_sigs, d_dom8s, b, s, &f, &st))) return rc;
+  LAUNCH_FE(s, n_calls, f, st, d_verdicts);
+  return keep_until_done(c, s, pl);
 } catch (const std::exception& e) {
   t_err = e.what();
   return BLS381_EARG;

@@ -179,6 +179,26 @@ int bls381_verify_multiple_batch_device(size_t n_calls, const uint32_t* h_call_o
                                         const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
                                         void* stream);
 
+/* Batched validate_indexed_attestation (reference 0_beacon-chain.md:1023-1026):
+ *   bls_verify_multiple(pubkeys=[bls_aggregate_pubkeys(group) for group in call c],
+ *                       message_hashes=[one message per group], signature, domain)
+ * in one call, with the aggregation fused in: call c owns groups
+ * [h_call_group_off[c], h_call_group_off[c+1]); group g owns the member keys
+ * d_pks[h_group_key_off[g] .. h_group_key_off[g+1]) (48 B each, device memory, in
+ * group order) and message h_group_msgs[g] (msg_len bytes, host).  The members' sum
+ * runs beside hash_to_G2 instead of before it.  An empty group is the infinite
+ * aggregate (its pairing is 1); groups of one call with equal messages are merged, as
+ * py_ecc's verify_multiple does.  Divergence: an undecodable member key makes the
+ * verdict 0 where bls_aggregate_pubkeys would raise.  Queued on `stream`, not
+ * synchronised; the workspace must hold bls381_verify_multiple_grouped_workspace_size. */
+size_t bls381_verify_multiple_grouped_workspace_size(size_t n_calls, size_t n_groups, size_t n_pks,
+                                                     size_t msg_len);
+int bls381_verify_multiple_grouped_device(size_t n_calls, const uint32_t* h_call_group_off, size_t n_groups,
+                                          const uint32_t* h_group_key_off, const uint8_t* h_group_msgs,
+                                          size_t msg_len, const uint8_t* d_pks, const uint8_t* d_sigs,
+                                          const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                          void* stream);
+
 /* ---- multi-GPU partial products --------------------------- */
 /* Miller-loop product of one shard of a bls_verify_multiple call: pairs
  * (hash_to_G2(msg_g), group_pubkey_g) for the messages in this shard, plus

@@ -791,6 +791,71 @@ def test_verify_multiple_batch_device_entry(native, golden, torsion):
     assert got == [int(e) for _, e in cases]
 
 
+def test_verify_multiple_grouped_device(native, golden, torsion):
+    """bls381_verify_multiple_grouped_device (validate_indexed_attestation's
+    verify_multiple-of-aggregates, aggregation fused): golden + torsion calls regrouped by
+    message, with one group split in two under the same message (merged again) and an empty
+    group per call (the infinite aggregate); per-call verdicts == the fixtures' py_ecc column,
+    and committee batches == bls381_verify_multiple_batch."""
+    import ctypes
+    import torch
+    from bls381_amd import bls
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    h = bytes.fromhex
+    _, gb = golden
+    cases = [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
+              c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+    cases += [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
+               c["expected_pyecc"]) for c in torsion["verify_multiple"]]
+    rng = random.Random(0xB15_0C0D)
+    sks = [rng.randrange(1, O.r) for _ in range(24)]
+    pubs = [bls.privtopub(k) for k in sks]
+    for members, ms, sig, dom, ok in _committee_calls(rng, 30, 10, sks):
+        cases.append(([pubs[i] for i in members], ms, sig, dom, ok))
+
+    def run(calls):
+        cgo, gko, gmsgs, keys, sigs, doms = [0], [0], [], [], b"", b""
+        for pks, ms, sig, dom, _ in calls:
+            order = []
+            for m in ms:
+                if m not in order:
+                    order.append(m)
+            groups = [[p for p, mm in zip(pks, ms) if mm == m] for m in order]
+            gm = list(order)
+            if groups and len(groups[0]) >= 2:            # split: two groups, same message
+                groups = [groups[0][:1], groups[0][1:]] + groups[1:]
+                gm = [gm[0], gm[0]] + gm[1:]
+            groups.append([])                             # the empty aggregate
+            gm.append(bytes(rng.getrandbits(8) for _ in range(32)))
+            for g, m in zip(groups, gm):
+                keys += g
+                gmsgs.append(m)
+                gko.append(gko[-1] + len(g))
+            cgo.append(cgo[-1] + len(groups))
+            sigs += sig
+            doms += dom.to_bytes(8, "big")
+        cgo = np.array(cgo, dtype=np.uint32)
+        gko = np.array(gko, dtype=np.uint32)
+        t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+        d_pks, d_sigs, d_doms = t(b"".join(keys) + b"\0"), t(sigs), t(doms)
+        d_v = torch.full((len(calls),), 7, dtype=torch.uint8, device=dev)
+        ws = torch.empty(L.bls381_verify_multiple_grouped_workspace_size(len(calls), len(gmsgs), len(keys), 32),
+                         dtype=torch.uint8, device=dev)
+        native.check(L.bls381_verify_multiple_grouped_device(
+            len(calls), cgo.ctypes.data_as(ctypes.c_void_p), len(gmsgs), gko.ctypes.data_as(ctypes.c_void_p),
+            b"".join(gmsgs), 32, d_pks.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(), d_v.data_ptr(),
+            ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        return [bool(x) for x in d_v.cpu().tolist()]
+
+    native.set_subgroup_policy("pyecc")
+    assert run(cases) == [bool(c[4]) for c in cases]
+    # one call per attestation, as an epoch: the same verdicts in a batch of 600 (task path)
+    many = [cases[i % len(cases)] for i in range(600)]
+    assert run(many) == [bool(c[4]) for c in many]
+
+
 # ------------------------------------ native multi-GPU ABI over RCCL (SURVEY §8e)
 def _comm_checks(native, golden, torsion):
     from bls381_amd import comm
