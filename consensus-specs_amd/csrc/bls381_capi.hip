@@ -426,6 +426,13 @@ struct VmPlan {
   // tasks are the quad_pair entries, and these passes multiply them per call
   bool tasks = false;
   std::vector<std::vector<agg_chunk>> task_passes;
+  // large batches: the signature pairs leave the quads (each call's group pairs fill whole
+  // quads; its signature pair runs on a side stream beside hash_to_G2).  Miller values sit
+  // in per-call slot ranges [quads of call c][signature of call c]: quad q writes slot
+  // quad_slot[q], call c's signature slot sig_slot[c] (task sig_task[c]); passes multiply them.
+  std::vector<uint32_t> quad_slot, sig_slot;
+  std::vector<int32_t> sig_task;
+  size_t nslots = 0;
   AggPlan agg;                                 // group pubkey sums over key_idx order
 };
 
@@ -478,6 +485,49 @@ uint64_t msg_hash(const uint8_t* m, size_t len) {
   for (size_t k = 0; i + k < len; ++k) t |= (uint64_t)m[i + k] << (8 * k);
   h = (h ^ t) * 0x94d049bb133111ebull;
   return h ^ (h >> 29);
+}
+
+// Shared tail of the planners: small batches run every pair (signatures included) as a
+// lane-quad task; large ones take the signature pairs out of the quads (VmPlan comments).
+void finish_plan(VmPlan& pl) {
+  const size_t n_calls = pl.n_calls;
+  pl.nquads = pl.quad_pair.size() / 2;
+  pl.tasks = 2 * pl.nquads <= BLS_VM_TASK_MAX;
+  if (pl.tasks) {
+    std::vector<uint32_t> toff(pl.call_quad_off.size());
+    for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
+    pl.task_passes = plan_products(toff);
+    return;
+  }
+  std::vector<int32_t> qp;
+  std::vector<uint32_t> cqo{0}, foff{0};
+  pl.sig_task.assign(n_calls, PAIR_NONE);
+  std::vector<int32_t> groups;
+  for (size_t c = 0; c < n_calls; ++c) {
+    groups.clear();
+    for (uint32_t e = 2 * pl.call_quad_off[c]; e < 2 * pl.call_quad_off[c + 1]; ++e) {
+      const int32_t v = pl.quad_pair[e];
+      if (v >= 0) groups.push_back(v);
+      else if (v != PAIR_NONE) pl.sig_task[c] = v;
+    }
+    for (size_t k = 0; k < groups.size(); k += 2) {
+      qp.push_back(groups[k]);
+      qp.push_back(k + 1 < groups.size() ? groups[k + 1] : PAIR_NONE);
+    }
+    cqo.push_back((uint32_t)(qp.size() / 2));
+    foff.push_back(cqo.back() + (uint32_t)(c + 1));
+  }
+  pl.quad_pair = std::move(qp);
+  pl.call_quad_off = std::move(cqo);
+  pl.nquads = pl.quad_pair.size() / 2;
+  pl.nslots = pl.nquads + n_calls;
+  pl.quad_slot.resize(pl.nquads);
+  pl.sig_slot.resize(n_calls);
+  for (size_t c = 0; c < n_calls; ++c) {
+    for (uint32_t q = pl.call_quad_off[c]; q < pl.call_quad_off[c + 1]; ++q) pl.quad_slot[q] = q + (uint32_t)c;
+    pl.sig_slot[c] = foff[c + 1] - 1;
+  }
+  pl.passes = plan_products(foff);
 }
 
 // Host plan of a verify_multiple batch: per call, pubkeys grouped by distinct message
@@ -546,14 +596,7 @@ VmPlan plan_vm(size_t n_calls, const uint32_t* call_off, const uint8_t* msgs, si
     }
     pl.call_quad_off.push_back((uint32_t)(pl.quad_pair.size() / 2));
   }
-  pl.nquads = pl.quad_pair.size() / 2;
-  if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
-  pl.tasks = 2 * pl.nquads <= BLS_VM_TASK_MAX;
-  if (pl.tasks) {
-    std::vector<uint32_t> toff(pl.call_quad_off.size());
-    for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
-    pl.task_passes = plan_products(toff);
-  }
+  finish_plan(pl);
   if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
   return pl;
 }
@@ -615,14 +658,7 @@ VmPlan plan_vm_grouped(size_t n_calls, const uint32_t* call_group_off, const uin
     }
     pl.call_quad_off.push_back((uint32_t)(pl.quad_pair.size() / 2));
   }
-  pl.nquads = pl.quad_pair.size() / 2;
-  if (pl.nquads > n_calls) pl.passes = plan_products(pl.call_quad_off);
-  pl.tasks = 2 * pl.nquads <= BLS_VM_TASK_MAX;
-  if (pl.tasks) {
-    std::vector<uint32_t> toff(pl.call_quad_off.size());
-    for (size_t k = 0; k < toff.size(); ++k) toff[k] = 2 * pl.call_quad_off[k];
-    pl.task_passes = plan_products(toff);
-  }
+  finish_plan(pl);
   if (pl.G) pl.agg = plan_agg(pl.G, pl.group_off.data());
   return pl;
 }
@@ -637,9 +673,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
                                                         const uint8_t* __restrict__ agg_st, size_t ncalls,
                                                         const uint32_t* __restrict__ sig_aff,
                                                         const uint8_t* __restrict__ sig_st,
+                                                        const uint32_t* __restrict__ slot, size_t nslots,
                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
   const size_t q = item_index<4>();
   if (q >= nq) return;
+  const size_t o = slot ? slot[q] : q;   // output slot (stride nslots)
   const bool hi = qd_hi();
   const bool lead = (threadIdx.x & 3u) == 0;
   const int p = pr_odd() ? 1 : 0;
@@ -653,7 +691,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
   const int32_t mine = quad_pair[2 * q + (hi ? 1 : 0)], other = quad_pair[2 * q + (hi ? 0 : 1)];
   bool bad_m, bad_o;
   const bool act_m = status(mine, bad_m), act_o = status(other, bad_o);
-  if (bad_m || bad_o) { if (lead) st_out[q] = ST_BAD; return; }   // same on all four lanes
+  if (bad_m || bad_o) { if (lead) st_out[o] = ST_BAD; return; }   // same on all four lanes
   fq12_t f;
   bool degen = false;
   if (act_m || act_o) {
@@ -675,12 +713,12 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
   } else {
     f = fq12_one();
   }
-  const size_t lp = 2 * q + p;
+  const size_t lp = 2 * o + p;
   const int c0 = hi ? 3 : 0;
-  soa_st(f_out, 2 * nq, lp, c0 + 0, f.h.c0.v);
-  soa_st(f_out, 2 * nq, lp, c0 + 1, f.h.c1.v);
-  soa_st(f_out, 2 * nq, lp, c0 + 2, f.h.c2.v);
-  if (lead) st_out[q] = degen ? ST_BAD : ST_OK;
+  soa_st(f_out, 2 * nslots, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * nslots, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * nslots, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[o] = degen ? ST_BAD : ST_OK;
 }
 
 // each lane multiplies one chunk [begin, end) of Fp12 values (statuses OR-ed);
@@ -696,16 +734,18 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
                                                            const uint8_t* __restrict__ agg_st, size_t ncalls,
                                                            const uint32_t* __restrict__ sig_aff,
                                                            const uint8_t* __restrict__ sig_st,
+                                                           const uint32_t* __restrict__ slot, size_t nslots,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
   const size_t t = item_index<4>();
   if (t >= nt) return;
   const bool lead = (threadIdx.x & 3u) == 0;
   const int p = pr_odd() ? 1 : 0;
   const int32_t src = tasks[t];
+  const size_t o = slot ? slot[t] : t;   // output slot (stride nslots)
   uint8_t sq = ST_INF, sp = ST_INF;
   if (src >= 0) { sq = h_st[src]; sp = agg_st[src]; }
   else if (src != PAIR_NONE) { sq = sig_st[(size_t)(-src - 1)]; sp = ST_OK; }
-  if (sq == ST_BAD || sp == ST_BAD) { if (lead) st_out[t] = ST_BAD; return; }
+  if (sq == ST_BAD || sp == ST_BAD) { if (lead) st_out[o] = ST_BAD; return; }
   fq12_t f;
   bool degen = false;
   if (sq == ST_OK && sp == ST_OK) {
@@ -725,12 +765,12 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
   } else {
     f = fq12_one();
   }
-  const size_t lp = 2 * t + p;
+  const size_t lp = 2 * o + p;
   const int c0 = qd_hi() ? 3 : 0;
-  soa_st(f_out, 2 * nt, lp, c0 + 0, f.h.c0.v);
-  soa_st(f_out, 2 * nt, lp, c0 + 1, f.h.c1.v);
-  soa_st(f_out, 2 * nt, lp, c0 + 2, f.h.c2.v);
-  if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
+  soa_st(f_out, 2 * nslots, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * nslots, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * nslots, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[o] = degen ? ST_BAD : ST_OK;
 }
 
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_fp12_chunk_product(size_t nchunks, const agg_chunk* __restrict__ chunks,
@@ -787,6 +827,20 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
   uint8_t* h_st = b.take<uint8_t>(G + 1);
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
+  // Miller values: one per pair task (small batches), or the quads' and the signatures' slots
+  const size_t nf = pl.tasks ? 2 * nq : pl.nslots;
+  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nf);
+  uint8_t* st = b.take<uint8_t>(nf);
+  uint32_t *d_qslot = nullptr, *d_sslot = nullptr;
+  int32_t* d_stask = nullptr;
+  if (!pl.tasks) {
+    d_qslot = b.take<uint32_t>(nq + 1);
+    d_sslot = b.take<uint32_t>(ncalls);
+    d_stask = b.take<int32_t>(ncalls);
+    if (nq) HIPC(hipMemcpyAsync(d_qslot, pl.quad_slot.data(), 4 * nq, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(d_sslot, pl.sig_slot.data(), 4 * ncalls, hipMemcpyHostToDevice, s));
+    HIPC(hipMemcpyAsync(d_stask, pl.sig_task.data(), 4 * ncalls, hipMemcpyHostToDevice, s));
+  }
   // Small batches (an epoch's attestations, one custody call) leave most of the
   // GPU idle, so the independent stages overlap: the pubkey-group sums and the
   // signature decodes run on the side stream while the main stream hashes the
@@ -817,6 +871,14 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
     LAUNCH("decode_g2", c->side2, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, d_sigs, sig_aff,
            sig_st, chk);
+    if (!pl.tasks) {
+      // large batches: the signature pairs run here, beside hash_to_G2, so the group pairs fill
+      // whole quads and the main Miller launch has no partial last round of waves
+      LAUNCH("miller_sig_tasks", c->side2, dim3(grid_for(4 * ncalls)), dim3(KBLOCK), k_miller_tasks_q1, ncalls,
+             (const int32_t*)d_stask, G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff,
+             (const uint8_t*)agg_st, ncalls, (const uint32_t*)sig_aff, (const uint8_t*)sig_st,
+             (const uint32_t*)d_sslot, nf, f, st);
+    }
     HIPC(hipEventRecord(c->ev_join2, c->side2));
     if (G > 0) {
       LAUNCH("gather_domains", s, dim3(grid_for(8 * G)), dim3(KBLOCK), k_gather_rows, G, (const uint32_t*)d_gcall,
@@ -827,17 +889,14 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
   }
-  const size_t nf = pl.tasks ? 2 * nq : nq;
-  uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nf);
-  uint8_t* st = b.take<uint8_t>(nf);
   if (pl.tasks) {
     LAUNCH("miller_tasks_q1", s, dim3(grid_for(4 * nf)), dim3(KBLOCK), k_miller_tasks_q1, nf, (const int32_t*)d_qp,
            G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
-           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, (const uint32_t*)nullptr, nf, f, st);
   } else {
     LAUNCH("miller_quads", s, dim3(grid_for(4 * nq)), dim3(KBLOCK), k_miller_quads, nq, (const int32_t*)d_qp, G,
            (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
-           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, f, st);
+           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, (const uint32_t*)d_qslot, nf, f, st);
   }
   // segmented products (chunk lists live in the plan, which outlives the stream work)
   size_t n_in = nf;
@@ -866,7 +925,7 @@ size_t vm_ws_bound(const VmPlan& pl, size_t mlen) {
   s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
   s += agg_ws_size(pl.agg, 3) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
-  s += align256(12 * FPW * 2 * nq) + align256(2 * nq);
+  s += align256(12 * FPW * (2 * nq + nc)) + align256(2 * nq + nc) + align256(4 * nq) + 2 * align256(4 * nc);
   for (const auto& ch : pl.tasks ? pl.task_passes : pl.passes)
     s += align256(ch.size() * sizeof(agg_chunk)) + align256(12 * FPW * ch.size()) + align256(ch.size());
   s += align256(nc);
@@ -885,7 +944,7 @@ size_t vm_ws_bound_sizes(size_t n_calls, size_t n_keys, size_t mlen) {
   s += 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks)) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
   // Miller values: quads, or two pair tasks per quad on the latency path
-  s += align256(12 * FPW * 2 * nq) + align256(2 * nq);
+  s += align256(12 * FPW * (2 * nq + nc)) + align256(2 * nq + nc) + align256(4 * nq) + 2 * align256(4 * nc);
   // product passes: <= nt / 8 + n_calls chunks per pass over nt <= 2 nq values, and the
   // sizes shrink 8x per pass
   const size_t pc = nq / 2 + 2 * nc;
