@@ -16,9 +16,11 @@ Also reported (secondary lines in the same JSON object):
 - "aggregation": committee pubkey aggregation alone (1024 committees x 128);
 - "c3_epoch": one epoch of attestations per GPU -- per committee
   bls_aggregate_pubkeys(128 pks) + bls_aggregate_pubkeys([]) +
-  bls_verify_multiple([agg, inf], [m0, m1], sig, 2), the aggregation on device
-  buffers and the 1024 verify_multiple calls as ONE batched call (host
-  buffers: host-side message grouping and PCIe copies are inside the time);
+  bls_verify_multiple([agg, inf], [m0, m1], sig, 2): the aggregation and the
+  1024 verify_multiple calls as two batched device calls (aggregates stay in
+  HBM); "grouped": the same epoch as one bls381_verify_multiple_grouped_device
+  call (validate_indexed_attestation's pattern, the sums beside hash_to_G2);
+  "grouped_registry": the same with members as registry entries;
 - "c4_aggregate": 2^17 pubkeys per GPU aggregated to one partial, partials
   all-gathered over RCCL and summed on rank 0 (2^20 keys at 8 GPUs);
 - "c5_multi_pairing": bls_verify_multiple with L distinct messages;
@@ -271,12 +273,42 @@ def bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist
         fused()
     torch.cuda.synchronize()
     tf = _max_time(time.perf_counter() - t1, world, dist, dev)
+    # and with the members as validator indices into a device pubkey registry (a node keeps the
+    # registry decoded; 0_beacon-chain.md:1025-1026 reads state.validator_registry[i].pubkey)
+    from bls381_amd.registry import PubkeyRegistry
+    reg = PubkeyRegistry(n)
+    ent = reg.add([pks[48 * i:48 * i + 48] for i in range(n)])
+    assert np.all(ent >= 0)
+    d_ent = t_u8(ent[idx].astype(np.uint32).tobytes())
+    d_ver3 = torch.zeros(nc, dtype=torch.uint8, device=dev)
+
+    def fused_reg():
+        native.check(L.bls381_registry_verify_multiple_grouped_device(
+            reg._h, nc, call_groups.ctypes.data_as(ctypes.c_void_p), 2 * nc, offsets.ctypes.data_as(ctypes.c_void_p),
+            msgs, 32, d_ent.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(), d_ver3.data_ptr(), gws.data_ptr(),
+            ctypes.c_void_p(stream.cuda_stream)))
+
+    fused_reg()
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ver3.cpu().numpy().astype(bool), expected), "C3 registry grouped verdict mismatch"
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(steps):
+        fused_reg()
+    torch.cuda.synchronize()
+    tr = _max_time(time.perf_counter() - t2, world, dist, dev)
+    reg.close()
     return {"workload": "C3: %d committees x %d per GPU: 2 x bls_aggregate_pubkeys + bls_verify_multiple([agg, inf], "
                         "[m0, m1], sig, 2) each, 1/16 wrong message; device-resident (aggregates never leave HBM)"
                         % (nc, cs),
             "attestations_per_s": nc * steps * world / t, "ms_per_epoch_step": 1e3 * t / steps, "n_gpus": world,
             "grouped": {"api": "bls381_verify_multiple_grouped_device (aggregation fused beside hash_to_G2)",
-                        "attestations_per_s": nc * steps * world / tf, "ms_per_epoch_step": 1e3 * tf / steps}}
+                        "attestations_per_s": nc * steps * world / tf, "ms_per_epoch_step": 1e3 * tf / steps},
+            "grouped_registry": {"api": "bls381_registry_verify_multiple_grouped_device (members as registry "
+                                        "entries of the %d keys)" % n,
+                                 "attestations_per_s": nc * steps * world / tr, "ms_per_epoch_step": 1e3 * tr / steps}}
 
 
 def bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8):

@@ -89,6 +89,9 @@ _SIGS = {
     "bls381_registry_destroy": (None, [ctypes.c_void_p]),
     "bls381_registry_size": (ctypes.c_size_t, [ctypes.c_void_p]),
     "bls381_registry_add": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_registry_verify_multiple_grouped_device": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, _u8p,
+                                                                      ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t,
+                                                                      _u8p, _u8p, _u8p, _u8p, _u8p, _u8p]),
     "bls381_registry_lookup": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, _u8p, _u8p]),
     "bls381_registry_aggregate_indices": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, _u8p, _u8p, _u8p,
                                                          _u8p]),

@@ -216,7 +216,7 @@ int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* 
 
 // ----------------------------------------------------- verify_batch (C2) --
 struct VerifyWs {
-  uint32_t *pk_aff, *sig_aff, *h_aff, *f;
+  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff;
   uint8_t *pk_st, *sig_st, *f_st;
 };
 // bls_verify batches of at most this many items run each Miller pair on its own lane
@@ -226,11 +226,16 @@ struct VerifyWs {
 #ifndef BLS_ML_OCT_MAX_N
 #define BLS_ML_OCT_MAX_N 8192
 #endif
+// hash_to_G2 of batches of at most this many messages runs the wide candidate search first
+// (k_hash_search: 16 lanes per message, one Legendre symbol each)
+#ifndef BLS_HASH_WIDE_MAX_N
+#define BLS_HASH_WIDE_MAX_N 8192
+#endif
 // Fp12 values the Miller stage of a verify batch writes (two per item on the octet path)
 size_t verify_nf(size_t n) { return n <= BLS_ML_OCT_MAX_N ? 2 * n : n; }
 size_t verify_ws_size(size_t n) {
   return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
-         align256(verify_nf(n)) + 1024;
+         align256(verify_nf(n)) + align256(4 * n) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n) {
   Bump b(ws);
@@ -242,6 +247,7 @@ VerifyWs carve_verify(void* ws, size_t n) {
   w.pk_st = b.take<uint8_t>(n);
   w.sig_st = b.take<uint8_t>(n);
   w.f_st = b.take<uint8_t>(verify_nf(n));
+  w.koff = b.take<uint32_t>(n);
   return w;
 }
 
@@ -278,7 +284,13 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   HIPC(hipEventRecord(c->ev_join, c->side));
   LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk);
 #endif
-  LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  // small batches: the wide search first (16 candidates per message in one round), so the
+  // hash does not wait for the batch's slowest sequential search
+  const bool wide = n <= BLS_HASH_WIDE_MAX_N;
+  if (wide)
+    LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
+  LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
+         (const uint32_t*)(wide ? w.koff : nullptr));
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   if (n <= BLS_ML_OCT_MAX_N) {
     // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
@@ -804,8 +816,11 @@ __global__ void __launch_bounds__(KBLOCK) k_gather_rows(size_t n, const uint32_t
 // signatures and domains are device buffers (d_pks indexed by the caller's key
 // numbering); the plan's own arrays are copied here.  Returns per-call Fp12
 // products and statuses (SoA over n_calls) on the device.
+// reg != nullptr: the member keys are registry entries (d_pks holds one int32 entry per key,
+// 4 bytes, numbered like the keys), summed from the registry's decoded points.
 int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, const uint8_t* d_sigs,
-                 const uint8_t* d_doms, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st) {
+                 const uint8_t* d_doms, Bump& b, hipStream_t s, uint32_t** out_f, uint8_t** out_st,
+                 const agg_reg_src* reg = nullptr) {
   const size_t G = pl.G, ncalls = pl.n_calls, nq = pl.nquads;
   const int chk = check_subgroups();   // STRICT: every member key and signature is checked
   uint32_t* d_kidx = b.take<uint32_t>(pl.key_idx.size() + 1);
@@ -825,6 +840,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
   uint8_t* agg_st = b.take<uint8_t>(G + 1);
   uint32_t* h_aff = b.take<uint32_t>(4 * FP_LIMBS * (G + 1));
   uint8_t* h_st = b.take<uint8_t>(G + 1);
+  uint32_t* d_koff = b.take<uint32_t>(G + 1);
   uint32_t* sig_aff = b.take<uint32_t>(4 * FP_LIMBS * ncalls);
   uint8_t* sig_st = b.take<uint8_t>(ncalls);
   // Miller values: one per pair task (small batches), or the quads' and the signatures' slots
@@ -853,13 +869,17 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     if (G > 0) {
       // members in group order, then group sums -> affine
       const size_t nk = pl.key_idx.size();
-      if (nk) LAUNCH("gather_pubkeys", side, dim3(grid_for(48 * nk)), dim3(KBLOCK), k_gather_rows, nk,
-                     (const uint32_t*)d_kidx, d_pks, 48u, d_gpks);
+      const uint32_t row = reg ? 4u : 48u;   // registry entries or compressed keys
+      if (nk) LAUNCH("gather_pubkeys", side, dim3(grid_for(row * nk)), dim3(KBLOCK), k_gather_rows, nk,
+                     (const uint32_t*)d_kidx, d_pks, row, d_gpks);
       const uint32_t* jac;
       const uint8_t* bad;
       size_t used = 0;
       uint8_t* sub = b.take<uint8_t>(0);
-      int rc = run_agg<fp_t>(pl.agg, G, d_gpks, sub, side, &jac, &bad, &used, b.left(), nullptr, chk);
+      agg_reg_src rs{};
+      if (reg) { rs = *reg; rs.entry = (const int32_t*)d_gpks; }
+      int rc = run_agg<fp_t>(pl.agg, G, reg ? nullptr : d_gpks, sub, side, &jac, &bad, &used, b.left(),
+                             reg ? &rs : nullptr, chk);
       if (rc) return rc;
       b.off += used;
       LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
@@ -883,8 +903,12 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     if (G > 0) {
       LAUNCH("gather_domains", s, dim3(grid_for(8 * G)), dim3(KBLOCK), k_gather_rows, G, (const uint32_t*)d_gcall,
              d_doms, 8u, d_gdom);
+      const bool wide = pl.tasks && G <= BLS_HASH_WIDE_MAX_N;
+      if (wide)
+        LAUNCH("hash_search", s, dim3(grid_for(16 * G)), dim3(KBLOCK), k_hash_search<16>, G, (const uint8_t*)d_gmsg,
+               (uint32_t)mlen, (const uint8_t*)d_gdom, 8, d_koff);
       LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
-             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st);
+             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr));
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -922,7 +946,7 @@ size_t vm_ws_bound(const VmPlan& pl, size_t mlen) {
   size_t s = 1 << 16;
   s += align256(4 * nk) + align256(G * mlen + 1) + align256(4 * G) + align256(8 * G + 1) + align256(48 * nk) +
        align256(8 * nq);
-  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
+  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G) + align256(4 * G);
   s += agg_ws_size(pl.agg, 3) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
   s += align256(12 * FPW * (2 * nq + nc)) + align256(2 * nq + nc) + align256(4 * nq) + 2 * align256(4 * nc);
@@ -938,7 +962,7 @@ size_t vm_ws_bound_sizes(size_t n_calls, size_t n_keys, size_t mlen) {
   size_t s = 1 << 16;
   s += align256(4 * nk) + align256(G * mlen + 1) + align256(4 * G) + align256(8 * G + 1) + align256(48 * nk) +
        align256(8 * nq);
-  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G);
+  s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G) + align256(4 * G);
   // group-sum levels: chunks <= groups + keys / CHUNK per level, three levels at most below 2^27 keys
   const size_t chunks = G + n_keys / CHUNK_L1 + 1;
   s += 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks)) + 256;
@@ -1703,6 +1727,42 @@ int bls381_registry_aggregate_indices_device(bls381_registry* reg, size_t n_grou
   return BLS381_EARG;
 }
 
+int bls381_registry_verify_multiple_grouped_device(bls381_registry* reg, size_t n_calls,
+                                                   const uint32_t* h_call_group_off, size_t n_groups,
+                                                   const uint32_t* h_group_key_off, const uint8_t* h_group_msgs,
+                                                   size_t msg_len, const uint32_t* d_entries, const uint8_t* d_sigs,
+                                                   const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                                   void* stream) try {
+  if (!reg) return BLS381_EARG;
+  if (n_calls == 0) return 0;
+  if (!h_call_group_off || !h_group_key_off || !d_sigs || !d_dom8s || !d_verdicts || !d_workspace ||
+      msg_len > BLS381_MSG_MAX)
+    return BLS381_EARG;
+  if (h_call_group_off[0] != 0 || h_call_group_off[n_calls] != n_groups || h_group_key_off[0] != 0) return BLS381_EARG;
+  for (size_t k = 0; k < n_calls; ++k)
+    if (h_call_group_off[k + 1] < h_call_group_off[k]) return BLS381_EARG;
+  for (size_t g = 0; g < n_groups; ++g)
+    if (h_group_key_off[g + 1] < h_group_key_off[g]) return BLS381_EARG;
+  const size_t nk = h_group_key_off[n_groups];
+  if ((nk && !d_entries) || (n_groups && msg_len && !h_group_msgs)) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = registry_ctx(reg, &rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> lr(reg->mu);
+  auto pl = std::make_shared<VmPlan>(plan_vm_grouped(n_calls, h_call_group_off, h_group_key_off, h_group_msgs, msg_len));
+  hipStream_t s = (hipStream_t)stream;
+  Bump b(d_workspace, bls381_verify_multiple_grouped_workspace_size(n_calls, n_groups, nk, msg_len));
+  const agg_reg_src src{nullptr, reg->aff, reg->st, reg->cap, reg->size};
+  uint32_t* f;
+  uint8_t* st;
+  if ((rc = run_vm_batch(c, *pl, msg_len, (const uint8_t*)d_entries, d_sigs, d_dom8s, b, s, &f, &st, &src))) return rc;
+  LAUNCH_FE(s, n_calls, f, st, d_verdicts);
+  return keep_until_done(c, s, pl);
+} catch (const std::exception& e) {
+  t_err = e.what();
+  return BLS381_EARG;
+}
+
 static int registry_agg_host(bls381_registry* reg, size_t ng, const uint32_t* offsets, const uint32_t* indices,
                              const uint8_t* pks, uint8_t* out48, int32_t* status) try {
   int rc = 0;
@@ -2326,7 +2386,8 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("rb_miller_sig", side, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, B, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, side));
-    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st);
+    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
+           (const uint32_t*)nullptr);
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
            (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);

@@ -147,19 +147,58 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n
 // (msg, dom8) -> the verification hash BP(H0) = [3(x^2-1)] hash_to_G2(msg, dom)
 // affine (pair SoA; g2_mul_bp: every verify kernel pairs it with the pubkey and
 // the signature with -[3(x^2-1)] g1, G1_VGEN_*).  dom_stride 0 = one shared domain.
+// koff != nullptr: the try-and-increment offsets k_hash_search found (no search here).
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                    const uint8_t* __restrict__ doms, int dom_stride,
-                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ st) {
+                                                   uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                   const uint32_t* __restrict__ koff) {
   const size_t i = item_index<2>();
   if (i >= n) return;
   uint8_t dom[8];
   ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
   aff_t<fp2p_t> c;
-  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, koff ? (int)koff[i] : -1);
   aff_t<fp2p_t> h;
   const bool fin = jac_to_aff(h, g2_mul_bp(c));
   if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
   if (fin) soa_st_g2(out, n, i, h);
+}
+
+// The latency form of the try-and-increment search (bls_signature.md:74-86): W lanes per
+// message test candidates x + k, x + k + 1, ..., one Legendre symbol each (one-lane Fp2
+// arithmetic), and the item's lowest square offset is taken from a ballot; with W = 16 a
+// round fails with probability 2^-16, so a batch no longer waits for its slowest item's
+// ~6 sequential rounds.  koff[i] = the offset of the first square (the spec's point).
+template <int W>
+__global__ void __launch_bounds__(KBLOCK) k_hash_search(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                       const uint8_t* __restrict__ doms, int dom_stride,
+                                                       uint32_t* __restrict__ koff) {
+  static_assert(W == 16, "lane groups of 16 within a wave");
+  const size_t i = item_index<W>();
+  if (i >= n) return;
+  const uint32_t j = threadIdx.x % W;
+  uint8_t dom[8];
+  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+  const uint8_t* msg = msgs + (size_t)mlen * i;
+  uint32_t d[8];
+  fp2_t x;
+  sha256_msg_dom_tag(d, msg, mlen, dom, 1);
+  x.c0 = fp_to_mont(fp_plain_from_digest(d));
+  sha256_msg_dom_tag(d, msg, mlen, dom, 2);
+  x.c1 = fp_to_mont(fp_plain_from_digest(d));
+  for (uint32_t t = 0; t < j; ++t) x.c0 = fp_add(x.c0, FP_ONE_M);
+  const fp_t step8 = fp_mul_small(FP_ONE_M, 8);
+  const uint32_t sh = (threadIdx.x & 63u) & ~(uint32_t)(W - 1);
+  for (uint32_t base = 0;; base += W) {
+    const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
+    const bool sq = fp_legendre(fp_add(fp_sqr(rhs.c0), fp_sqr(rhs.c1))) >= 0;
+    const uint32_t m = (uint32_t)(__builtin_amdgcn_ballot_w64(sq) >> sh) & ((1u << W) - 1u);
+    if (m) {
+      if (j == 0) koff[i] = base + (uint32_t)__builtin_ctz(m);
+      break;
+    }
+    x.c0 = fp_add(fp_add(x.c0, step8), step8);
+  }
 }
 
 // --------------------------------------------------------- verify kernels --

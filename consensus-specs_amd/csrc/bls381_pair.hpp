@@ -302,8 +302,10 @@ __device__ inline void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
 // ------------------------------------------------------------ hash_to_G2 --
 // try-and-increment (bls_signature.md:74-86) before the cofactor: the even lane
 // hashes m || dom8 || 0x01 (x_re), the odd lane m || dom8 || 0x02 (x_im).
+// known_k >= 0: the candidate offset is already known (k_hash_search found the first
+// square, x + known_k), so the Legendre search is skipped.
 __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* msg, uint32_t mlen,
-                                           const uint8_t dom8[8]) {
+                                           const uint8_t dom8[8], int known_k = -1) {
   const bool odd = pr_odd();
   uint32_t d[8];
   sha256_msg_dom_tag(d, msg, mlen, dom8, odd ? 2 : 1);
@@ -319,7 +321,12 @@ __device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* ms
   // sequential Legendre evaluations.
   int trials = 0;
   fp2p_t rhs;
-  while (true) {
+  if (known_k >= 0) {
+    for (int j = 0; j < known_k; ++j) x.v = fp_add(x.v, inc);
+    rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));
+    trials = known_k + 1;
+  }
+  while (known_k < 0) {
     trials += 2;
     const fp2p_t x1 = pr_make(fp_add(x.v, inc));
     const fp2p_t r0 = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));

@@ -280,6 +280,19 @@ int bls381_registry_aggregate_indices_device(bls381_registry* reg, size_t n_grou
                                              size_t n_idx, const uint32_t* d_indices, uint8_t* d_out48,
                                              int32_t* d_status, void* d_workspace, void* stream);
 
+/* bls381_verify_multiple_grouped_device with the member keys given as registry entries
+ * (d_entries: one uint32 entry per member, in group order; the reference's
+ * state.validator_registry[i].pubkey, 0_beacon-chain.md:1025-1026): the committee sums
+ * add decoded registry points instead of decoding every member.  An entry past the
+ * registry's end, or one holding an undecodable key, makes the verdict 0.  Workspace:
+ * bls381_verify_multiple_grouped_workspace_size. */
+int bls381_registry_verify_multiple_grouped_device(bls381_registry* reg, size_t n_calls,
+                                                   const uint32_t* h_call_group_off, size_t n_groups,
+                                                   const uint32_t* h_group_key_off, const uint8_t* h_group_msgs,
+                                                   size_t msg_len, const uint32_t* d_entries, const uint8_t* d_sigs,
+                                                   const uint8_t* d_dom8s, uint8_t* d_verdicts, void* d_workspace,
+                                                   void* stream);
+
 /* ---- SSZ roots: the message_hash producer ---------- */
 /* hash_tree_root / signing_root of n serialized fixed-size SSZ items
  * (test_libs/pyspec/eth2spec/utils/ssz/ssz_impl.py:143-163, merkle_minimal.py

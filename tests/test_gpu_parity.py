@@ -815,7 +815,7 @@ def test_verify_multiple_grouped_device(native, golden, torsion):
     for members, ms, sig, dom, ok in _committee_calls(rng, 30, 10, sks):
         cases.append(([pubs[i] for i in members], ms, sig, dom, ok))
 
-    def run(calls):
+    def run(calls, reg=None):
         cgo, gko, gmsgs, keys, sigs, doms = [0], [0], [], [], b"", b""
         for pks, ms, sig, dom, _ in calls:
             order = []
@@ -843,10 +843,19 @@ def test_verify_multiple_grouped_device(native, golden, torsion):
         d_v = torch.full((len(calls),), 7, dtype=torch.uint8, device=dev)
         ws = torch.empty(L.bls381_verify_multiple_grouped_workspace_size(len(calls), len(gmsgs), len(keys), 32),
                          dtype=torch.uint8, device=dev)
-        native.check(L.bls381_verify_multiple_grouped_device(
-            len(calls), cgo.ctypes.data_as(ctypes.c_void_p), len(gmsgs), gko.ctypes.data_as(ctypes.c_void_p),
-            b"".join(gmsgs), 32, d_pks.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(), d_v.data_ptr(),
-            ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        if reg is None:
+            native.check(L.bls381_verify_multiple_grouped_device(
+                len(calls), cgo.ctypes.data_as(ctypes.c_void_p), len(gmsgs), gko.ctypes.data_as(ctypes.c_void_p),
+                b"".join(gmsgs), 32, d_pks.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(), d_v.data_ptr(),
+                ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
+        else:
+            # members as registry entries (an undecodable key's entry holds a BAD status)
+            ent = reg.add(keys) if keys else np.zeros(0, dtype=np.int32)
+            d_ent = t(ent.astype(np.int32).tobytes() + b"\0\0\0\0")
+            native.check(L.bls381_registry_verify_multiple_grouped_device(
+                reg._h, len(calls), cgo.ctypes.data_as(ctypes.c_void_p), len(gmsgs),
+                gko.ctypes.data_as(ctypes.c_void_p), b"".join(gmsgs), 32, d_ent.data_ptr(), d_sigs.data_ptr(),
+                d_doms.data_ptr(), d_v.data_ptr(), ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
         return [bool(x) for x in d_v.cpu().tolist()]
 
     native.set_subgroup_policy("pyecc")
@@ -854,6 +863,12 @@ def test_verify_multiple_grouped_device(native, golden, torsion):
     # one call per attestation, as an epoch: the same verdicts in a batch of 600 (task path)
     many = [cases[i % len(cases)] for i in range(600)]
     assert run(many) == [bool(c[4]) for c in many]
+    from bls381_amd.registry import PubkeyRegistry
+    reg = PubkeyRegistry(4096)
+    try:
+        assert run(cases, reg) == [bool(c[4]) for c in cases]
+    finally:
+        reg.close()
 
 
 # ------------------------------------ native multi-GPU ABI over RCCL
