@@ -50,7 +50,10 @@ struct Ctx {
   hipStream_t stream = nullptr;
   // side stream + fork/join events: independent stages of one batch run concurrently
   hipStream_t side = nullptr, side2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+  // high-priority stream: small latency-bound launches whose waves should be dispatched
+  // ahead of a large launch queued at the same time on another stream
+  hipStream_t prio = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr, ev_a = nullptr, ev_b = nullptr;
   std::mutex fork_mu;
   void* ws = nullptr;
   size_t ws_cap = 0;
@@ -105,12 +108,17 @@ Ctx* get_ctx(int* rc) {
     }
     Ctx* c = new Ctx();
     c->device = dev;
+    int prio_lo = 0, prio_hi = 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess ||
+        hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->prio, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_a, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_b, hipEventDisableTiming) != hipSuccess) {
       delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
     }
     g_ctx[dev] = c;
@@ -290,7 +298,7 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   if (wide)
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
   LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
-         (const uint32_t*)(wide ? w.koff : nullptr));
+         (const uint32_t*)(wide ? w.koff : nullptr), 0);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   if (n <= BLS_ML_OCT_MAX_N) {
     // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
@@ -908,7 +916,8 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
         LAUNCH("hash_search", s, dim3(grid_for(16 * G)), dim3(KBLOCK), k_hash_search<16>, G, (const uint8_t*)d_gmsg,
                (uint32_t)mlen, (const uint8_t*)d_gdom, 8, d_koff);
       LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
-             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr));
+             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr),
+             pl.tasks ? 1 : 0);
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -1011,11 +1020,15 @@ void bls381_shutdown(void) {
     (void)hipStreamDestroy(c->stream);
     (void)hipStreamSynchronize(c->side);
     (void)hipStreamSynchronize(c->side2);
+    (void)hipStreamSynchronize(c->prio);
     (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->side2);
+    (void)hipStreamDestroy(c->prio);
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipEventDestroy(c->ev_join2);
+    (void)hipEventDestroy(c->ev_a);
+    (void)hipEventDestroy(c->ev_b);
     delete c;
   }
   g_ctx.clear();
@@ -2362,39 +2375,41 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   uint32_t* s_aff = b.take<uint32_t>(4 * FP_LIMBS * nb);
   uint8_t* s_st = b.take<uint8_t>(nb);
   {
-    // side stream: decodes, then the whole signature branch ([r_i] sig_i, the sub-batch sums
-    // and their Miller loops on lane quads); main stream: hash_to_G2, [r_i] pk_i and the
-    // per-item Miller loops.  The branches join before the segmented products.
+    // Order: the signature branch first ([r_i] sig_i and the sub-batch sums, throughput
+    // launches on the main stream), then its 1,024-odd latency-bound sum Miller loops on
+    // the high-priority stream beside hash_to_G2 (their waves are dispatched first, the
+    // hash fills the rest of the chip), then [r_i] pk_i and the per-item loops, which join
+    // the sums' loops before the segmented products.  Everything else runs in sequence:
+    // the launches are whole rounds of waves (2n lanes, or n for the one-lane kernels), and
+    // overlapping two of them (decode_g1 beside decode_g2, [r_i] pk_i beside [r_i] sig_i)
+    // measured slower -- a second, partial round.
     std::lock_guard<std::mutex> lk(c->fork_mu);
-    hipStream_t side = c->side;
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(side, c->ev_fork, 0));
-    LAUNCH("decode_g1", side, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    LAUNCH("decode_g1", s, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
     // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-    LAUNCH("decode_g2", side, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
-    HIPC(hipEventRecord(c->ev_join, side));
-    LAUNCH("rb_scale_g2", side, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
+    LAUNCH("decode_g2", s, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
+    LAUNCH("rb_scale_g2", s, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
            (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
     const uint32_t* sjac;
     const uint8_t* sbad;
     size_t used = 0;
     uint8_t* sub = b.take<uint8_t>(0);
-    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, side, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
+    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, s, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
       return e;
     b.off += used;
-    LAUNCH("agg_g2_affine", side, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
-    LAUNCH("rb_miller_sig", side, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, B, (const uint32_t*)s_aff,
+    LAUNCH("agg_g2_affine", s, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(c->prio, c->ev_fork, 0));
+    LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, B, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
-    HIPC(hipEventRecord(c->ev_join2, side));
+    HIPC(hipEventRecord(c->ev_join2, c->prio));
     LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
-           (const uint32_t*)nullptr);
-    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+           (const uint32_t*)nullptr, 0);
     LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
            (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
+    HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
     LAUNCH("rb_miller_items", s, dim3(grid_for(2 * nb * B)), blk, k_rb_miller_items, n, B, nb * B,
            (const uint32_t*)w.h_aff, (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st,
            (const uint8_t*)cls, nslots, f, fst);
-    HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
   }
   int rc = 0;
   std::vector<uint32_t> seg(nb + 1);

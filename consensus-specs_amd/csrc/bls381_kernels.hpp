@@ -148,10 +148,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n
 // affine (pair SoA; g2_mul_bp: every verify kernel pairs it with the pubkey and
 // the signature with -[3(x^2-1)] g1, G1_VGEN_*).  dom_stride 0 = one shared domain.
 // koff != nullptr: the try-and-increment offsets k_hash_search found (no search here).
+// prio != 0: raise the waves' issue priority (s_setprio) -- the latency path, where a few
+// hash waves share SIMDs with a full-chip side launch (a grouped call's committee sums).
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
                                                    const uint8_t* __restrict__ doms, int dom_stride,
                                                    uint32_t* __restrict__ out, uint8_t* __restrict__ st,
-                                                   const uint32_t* __restrict__ koff) {
+                                                   const uint32_t* __restrict__ koff, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
   const size_t i = item_index<2>();
   if (i >= n) return;
   uint8_t dom[8];
