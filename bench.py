@@ -130,6 +130,41 @@ def load_pmc_traffic(prof_key, n):
     return None, None
 
 
+def issue_roofline(prof_key, n, measured_ms):
+    """Instruction-issue roofline of a kernel: its VALU instructions per launch from the
+    newest committed PMC pass (SQ_INSTS_VALU, _INT64, _INT32; wave instructions), each class priced at
+    its measured chip-wide issue rate (profiles/valu_peak_r02.json: v_mad_u64_u32 for INT64, v_add_u32 for
+    INT32, the median VOP3 rate for the rest), against the launch's live HIP-event time.  frac near 1
+    means the kernel issues VALU work back to back; the MAC-peak frac above is then bounded by the
+    representation (392 issued MACs per 300-MAC Fp product) and the non-MAC instructions."""
+    import glob
+    try:
+        rates = json.load(open(VALU_PEAK_FILE))
+    except Exception:
+        return None
+    vop3 = sorted(v for k, v in rates.items() if k.endswith("_Tops") and k not in (
+        "v_mad_u64_u32_Tops", "v_add_u32_Tops", "v_and_b32_Tops", "v_cmp+v_cndmask_Tops"))
+    r_other = vop3[len(vop3) // 2]
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_counters.json")))):
+        try:
+            k = json.load(open(f))["kernels"][PROFILE_KERNEL[prof_key]]
+            if int(k.get("waves", 0)) * 64 not in (n, 2 * n) or k.get("valu_int64_insts") is None:
+                continue
+            i64, i32 = k["valu_int64_insts"], k["valu_int32_insts"]
+            other = k["valu_insts"] - i64 - i32
+            model_ms = 64e3 * (i64 / (rates["v_mad_u64_u32_Tops"] * 1e12) + i32 / (rates["v_add_u32_Tops"] * 1e12) +
+                               other / (r_other * 1e12))
+            return {"kernel": PROFILE_KERNEL[prof_key], "valu_int64_insts": i64, "valu_int32_insts": i32,
+                    "valu_other_insts": other, "issue_time_ms": round(model_ms, 3),
+                    "measured_ms": round(measured_ms, 3), "frac": round(model_ms / measured_ms, 4),
+                    "rates_Tops": {"int64": rates["v_mad_u64_u32_Tops"], "int32": rates["v_add_u32_Tops"],
+                                   "other (median VOP3)": r_other},
+                    "source": os.path.relpath(f, ROOT)}
+        except Exception:
+            continue
+    return None
+
+
 def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
     """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build
     (strict = 1: with the subgroup checks of BLS381_POLICY_STRICT)."""
@@ -823,6 +858,7 @@ def main():
     whole = sum(counts.values()) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
     roofline["pipeline_achieved"] = round(whole, 3)
     roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
+    roofline["issue"] = issue_roofline(dom_k, n, kern_ms[dom_k])
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
