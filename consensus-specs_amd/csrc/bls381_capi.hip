@@ -53,7 +53,7 @@ struct Ctx {
   // high-priority stream: small latency-bound launches whose waves should be dispatched
   // ahead of a large launch queued at the same time on another stream
   hipStream_t prio = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr, ev_a = nullptr, ev_b = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
   std::mutex fork_mu;
   void* ws = nullptr;
   size_t ws_cap = 0;
@@ -116,9 +116,7 @@ Ctx* get_ctx(int* rc) {
         hipStreamCreateWithPriority(&c->prio, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_a, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_b, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
       delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
     }
     g_ctx[dev] = c;
@@ -1027,8 +1025,6 @@ void bls381_shutdown(void) {
     (void)hipEventDestroy(c->ev_fork);
     (void)hipEventDestroy(c->ev_join);
     (void)hipEventDestroy(c->ev_join2);
-    (void)hipEventDestroy(c->ev_a);
-    (void)hipEventDestroy(c->ev_b);
     delete c;
   }
   g_ctx.clear();
