@@ -27,6 +27,7 @@ _u8p = ctypes.c_void_p
 _SIGS = {
     "bls381_device_count": (ctypes.c_int, []),
     "bls381_init": (ctypes.c_int, [ctypes.c_int]),
+    "bls381_init_devices": (ctypes.c_int, [ctypes.c_int]),
     "bls381_shutdown": (None, []),
     "bls381_last_error": (ctypes.c_char_p, []),
     "bls381_set_subgroup_policy": (ctypes.c_int, [ctypes.c_int]),
@@ -37,6 +38,8 @@ _SIGS = {
     "bls381_verify_multiple": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]),
     "bls381_aggregate_pubkeys": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
     "bls381_aggregate_signatures": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_aggregate_g1": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_aggregate_g2": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
     "bls381_sign": (ctypes.c_int, [_u8p, ctypes.c_size_t, _u8p, _u8p, _u8p]),
     "bls381_privtopub": (ctypes.c_int, [_u8p, _u8p]),
     "bls381_sign_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p]),

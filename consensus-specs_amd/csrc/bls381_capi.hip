@@ -1005,6 +1005,18 @@ int bls381_init(int device) {
   return c ? 0 : rc;
 }
 
+int bls381_init_devices(int n_devices) {
+  const int cnt = bls381_device_count();
+  if (cnt <= 0) { t_err = "no HIP device"; return BLS381_ENODEV; }
+  if (n_devices < 1 || n_devices > cnt) { t_err = "device count out of range"; return BLS381_EARG; }
+  const int keep = t_device;
+  for (int d = n_devices - 1; d >= 0; --d) {
+    const int rc = bls381_init(d);
+    if (rc) return rc;
+  }
+  return keep >= 0 && keep < n_devices ? bls381_init(keep) : 0;   // device 0 stays selected otherwise
+}
+
 void bls381_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (Ctx* c : g_ctx) {
@@ -1421,6 +1433,11 @@ int bls381_aggregate_signatures(size_t n, const uint8_t* sigs, uint8_t out[96]) 
   int32_t st = 0;
   int rc = agg_host(1, 1, off, sigs, out, &st);
   return rc ? rc : st;
+}
+
+int bls381_aggregate_g1(size_t n, const uint8_t* pks, uint8_t out[48]) { return bls381_aggregate_pubkeys(n, pks, out); }
+int bls381_aggregate_g2(size_t n, const uint8_t* sigs, uint8_t out[96]) {
+  return bls381_aggregate_signatures(n, sigs, out);
 }
 
 // ---- single-item helpers (fixtures / reference API)

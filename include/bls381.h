@@ -55,6 +55,9 @@ int bls381_device_count(void);
 /* Select the device used by subsequent calls from this thread and create its
  * context (stream, workspace).  Idempotent. */
 int bls381_init(int device);
+/* Create the contexts of devices 0 .. n_devices-1 (SURVEY §8(b)'s bls381_init(n_devices);
+ * a process driving several GPUs then selects one per thread with bls381_init). */
+int bls381_init_devices(int n_devices);
 void bls381_shutdown(void);
 /* Last HIP error string of this thread (static storage). */
 const char* bls381_last_error(void);
@@ -86,6 +89,9 @@ int bls381_aggregate_pubkeys(size_t n, const uint8_t* pks, uint8_t out[48]);
 
 /* bls_aggregate_signatures (bls.py:39-41): sum of n G2 points. */
 int bls381_aggregate_signatures(size_t n, const uint8_t* sigs, uint8_t out[96]);
+/* SURVEY §8(b)'s names for the two aggregations (same behaviour). */
+int bls381_aggregate_g1(size_t n, const uint8_t* pks, uint8_t out[48]);
+int bls381_aggregate_g2(size_t n, const uint8_t* sigs, uint8_t out[96]);
 
 /* bls_sign (bls.py:44-46): [sk] hash_to_G2(msg, domain); sk 32-byte big-endian. */
 int bls381_sign(const uint8_t* msg, size_t msg_len, const uint8_t sk[32], const uint8_t dom8[8],

@@ -103,6 +103,26 @@ def test_golden_aggregates(native, golden):
         assert bls.bls_aggregate_signatures([bytes.fromhex(s) for s in it["input"]]).hex() == it["output"], it["kind"]
 
 
+def test_survey_abi_names(native, golden):
+    """SURVEY §8(b)'s names: bls381_init_devices(n) and bls381_aggregate_g1/_g2 behave as
+    bls381_init / bls381_aggregate_pubkeys / _signatures."""
+    import ctypes
+    L = native.lib()
+    assert L.bls381_init_devices(1) == 0
+    assert L.bls381_init_devices(0) != 0
+    _, gb = golden
+    for it in gb["aggregate_pubkeys"]:
+        pks = b"".join(bytes.fromhex(p) for p in it["input"])
+        out = ctypes.create_string_buffer(48)
+        assert L.bls381_aggregate_g1(len(it["input"]), pks, out) == 0
+        assert out.raw.hex() == it["output"], it["kind"]
+    for it in gb["aggregate_sigs"]:
+        sigs = b"".join(bytes.fromhex(p) for p in it["input"])
+        out = ctypes.create_string_buffer(96)
+        assert L.bls381_aggregate_g2(len(it["input"]), sigs, out) == 0
+        assert out.raw.hex() == it["output"], it["kind"]
+
+
 def test_golden_hash_to_g2(native, golden):
     from bls381_amd import bls
     _, gb = golden
