@@ -275,6 +275,9 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   VerifyWs w = carve_verify(ws, n);
   const dim3 g(grid_for(n)), g2(grid_for(2 * n)), b(KBLOCK);   // G1: lane per item; G2/Fp12: lane pair
   const int chk = check_subgroups();
+  // throughput path under the strict policy: the signature's G2 test moves from decode_g2 into
+  // the Miller loop, which computes [|x|] sig anyway (k_miller_verify's sig_check)
+  const bool sig_in_loop = chk && n > BLS_ML_QUAD_MAX_N;
   std::lock_guard<std::mutex> lk(c->fork_mu);
   // decode_g1 (one lane per item: one wave per SIMD) and, by default, decode_g2
   // on the side stream, beside hash_to_g2; the Miller loop waits for both branches.
@@ -284,11 +287,11 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
 #if BLS_DECODE_G2_SIDE
   // both decodes in sequence beside hash_to_G2
-  LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk);
+  LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
   HIPC(hipEventRecord(c->ev_join, c->side));
-  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk);
+  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
 #endif
   // small batches: the wide search first (16 candidates per message in one round), so the
   // hash does not wait for the batch's slowest sequential search
@@ -315,7 +318,8 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
            w.f, w.f_st);
   } else {
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
-           (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st);
+           (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st,
+           sig_in_loop ? 1 : 0);
   }
   LAUNCH_FE(s, n, w.f, w.f_st, verdicts);
   return 0;

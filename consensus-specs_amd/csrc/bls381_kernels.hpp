@@ -207,12 +207,16 @@ __global__ void __launch_bounds__(KBLOCK) k_hash_search(size_t n, const uint8_t*
 // --------------------------------------------------------- verify kernels --
 // One bls_verify per lane pair: FE( ML(sig, -g1) * ML(H(m), pk) ) == 1, with the
 // infinity short-circuit of py_ecc's pairing (a pair with an infinite point is 1).
+// sig_check (STRICT policy): the signature's G2 membership is tested here, on the loop's
+// final running point T = [|x|] sig (psi(sig) == -T), instead of by 64 more doublings in
+// k_decode_g2; a signature outside G2 makes the verdict False either way.
 __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(size_t n, const uint32_t* __restrict__ sig_aff,
                                                          const uint8_t* __restrict__ sig_st,
                                                          const uint32_t* __restrict__ pk_aff,
                                                          const uint8_t* __restrict__ pk_st,
                                                          const uint32_t* __restrict__ h_aff,
-                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out,
+                                                         int sig_check) {
   const size_t i = item_index<2>();
   if (i >= n) return;
   const bool lead = !pr_odd();
@@ -234,12 +238,15 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(s
   }
   fp12p_t f;
   bool degen = false;
-  if (np == 2) f = miller_loop_n<2>(Q, P, degen);
-  else if (np == 1) f = miller_loop_n<1>(Q, P, degen);
+  g2_proj<fp2p_t> T0;
+  g2_proj<fp2p_t>* t0 = (sig_check && ss == ST_OK) ? &T0 : nullptr;
+  if (np == 2) f = miller_loop_n<2>(Q, P, degen, t0);
+  else if (np == 1) f = miller_loop_n<1>(Q, P, degen, t0);
   else f = fp12_one<fp2p_t>();
+  bool bad = degen;   // a degenerate loop is py_ecc's zero pairing value: verdict False
+  if (t0 && !degen) bad = !g2_psi_matches_neg(Q[0], T0);
   soa_st12(f_out, n, i, f);
-  // a degenerate loop is py_ecc's zero pairing value: verdict False
-  if (lead) st_out[i] = degen ? ST_BAD : ST_OK;
+  if (lead) st_out[i] = bad ? ST_BAD : ST_OK;
 }
 
 // The same verify on a lane quad (bls381_quad.hpp): the lo half runs the pair

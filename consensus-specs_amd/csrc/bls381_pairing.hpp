@@ -87,8 +87,12 @@ BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre&
 // step.  py_ecc's Miller loop then doubles the point at infinity, whose line
 // has a zero denominator, so its pairing value is 0 and the verdict False; the
 // kernels map the flag to that verdict.  Points of G2 never reach it.
+// T0_out != nullptr: receives the first pair's final running point, [|x|] Q[0] in
+// homogeneous projective coordinates (the signature's G2 membership test rides on it,
+// g2_psi_matches_neg).
 template <int N, class E>
-BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bool& degenerate) {
+BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bool& degenerate,
+                                     g2_proj<E>* T0_out = nullptr) {
   g2_proj<E> T[N];
   for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = e2_one<E>(); }
   fp12_g<E> f = fp12_one<E>();
@@ -112,7 +116,18 @@ BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bo
   bool deg = false;
   for (int k = 0; k < N; ++k) deg = deg | fp2_is_zero(T[k].z);   // no short circuit: pair-uniform DPP
   degenerate = deg;
+  if (T0_out) *T0_out = T[0];
   return fp12_conj(f);
+}
+
+// G2 membership from a Miller loop's by-product: Q in G2 iff psi(Q) == [x] Q = -[|x|] Q, and
+// the loop's final running point T (homogeneous projective, Z != 0) is [|x|] Q.
+template <class E>
+BLS_HD inline bool g2_psi_matches_neg(const aff_t<E>& q, const g2_proj<E>& T) {
+  const aff_t<E> s = g2_psi(q);
+  const bool a = fp2_eq(fp2_mul(s.x, T.z), T.x);
+  const bool b = fp2_eq(fp2_mul(s.y, T.z), fp2_neg(T.y));
+  return a & b;
 }
 
 // runtime pair count (for verify_multiple chunks); pairs processed one at a time
