@@ -74,6 +74,62 @@ BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre&
   T = R;
 }
 
+// Two lines of one Miller step multiplied together before they meet f:
+//   l = (c0 + c1 v) + (c2 v) w,  l' = (d0 + d1 v) + (d2 v) w
+//   l l' = (t0 + xi s + m v + t1 v^2) + ((u - t0 - s) v + (u' - t1 - s) v^2) w
+// with t0 = c0 d0, t1 = c1 d1, s = c2 d2, m = (c0 + c1)(d0 + d1) - t0 - t1,
+// u = (c0 + c2)(d0 + d2), u' = (c1 + c2)(d1 + d2): 6 Fp2 products, and the product
+// has no w v^0 coefficient (fp12_mul_by_line_pair_inl uses that).
+template <class E>
+BLS_INLINE fp12_g<E> line_pair_product(const E& c0, const E& c1, const E& c2,
+                                       const E& d0, const E& d1, const E& d2) {
+  const E t0 = fp2_mul(c0, d0);
+  const E t1 = fp2_mul(c1, d1);
+  const E s = fp2_mul(c2, d2);
+  fp12_g<E> L;
+  L.c0.c0 = fp2_add_mul_xi(t0, s);
+  L.c0.c1 = fp2_sub2(fp2_mul(fp2_add_lazy(c0, c1), fp2_add_lazy(d0, d1)), t0, t1);
+  L.c0.c2 = t1;
+  L.c1.c0 = e2_zero<E>();
+  L.c1.c1 = fp2_sub2(fp2_mul(fp2_add_lazy(c0, c2), fp2_add_lazy(d0, d2)), t0, s);
+  L.c1.c2 = fp2_sub2(fp2_mul(fp2_add_lazy(c1, c2), fp2_add_lazy(d1, d2)), t1, s);
+  return L;
+}
+
+// f * L for L = P + Q w with Q = q1 v + q2 v^2 (line_pair_product's shape): 6 + 5 + 6 = 17
+// Fp2 products, against 2 x 13 for the two lines one at a time.
+template <class E>
+BLS_INLINE fp12_g<E> fp12_mul_by_line_pair_inl(const fp12_g<E>& f, const fp12_g<E>& L) {
+  const fp6_g<E>& a = f.c0;
+  const fp6_g<E>& b = f.c1;
+  const fp6_g<E> aP = fp6_mul_inl(a, L.c0);
+  // b Q: v^0 xi (b1 q2 + b2 q1), v^1 b0 q1 + xi b2 q2, v^2 b0 q2 + b1 q1
+  fp6_g<E> bQ;
+  {
+    const E t1 = fp2_mul(b.c1, L.c1.c1);
+    const E t2 = fp2_mul(b.c2, L.c1.c2);
+    bQ.c0 = fp2_mul_xi(fp2_sub2(fp2_mul(fp2_add_lazy(b.c1, b.c2), fp2_add_lazy(L.c1.c1, L.c1.c2)), t1, t2));
+    bQ.c1 = fp2_add_mul_xi(fp2_mul(b.c0, L.c1.c1), t2);
+    bQ.c2 = fp2_add(fp2_mul(b.c0, L.c1.c2), t1);
+  }
+  fp6_g<E> pq;
+  pq.c0 = L.c0.c0;
+  pq.c1 = fp2_add(L.c0.c1, L.c1.c1);
+  pq.c2 = fp2_add(L.c0.c2, L.c1.c2);
+  const fp6_g<E> m = fp6_mul_inl(fp6_add(a, b), pq);
+  fp12_g<E> r;
+  r.c0 = fp6_add_mul_by_v(aP, bQ);
+  r.c1 = fp6_sub2(m, aP, bQ);
+  return r;
+}
+
+// BLS_ML_LINE_PAIR=1: miller_loop_n multiplies the lines of pairs k, k+1 together first
+// (23 instead of 26 Fp2 products per step).  Off: on k_miller_verify it measured 14.15 ms
+// against 13.97 ms, same box, alternating runs (the product's live set adds spills).
+#ifndef BLS_ML_LINE_PAIR
+#define BLS_ML_LINE_PAIR 0
+#endif
+
 // Multi-Miller loop over n pairs (Q_k affine in G2, P_k affine in G1), all finite.
 // Returns conj(prod_k f_{|x|,Q_k}(P_k)) = prod_k f_{x,Q_k}(P_k) up to factors the
 // final exponentiation removes.  Squarings of f are shared by all pairs.
@@ -99,14 +155,32 @@ BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bo
   bool first = true;
   for (int i = 62; i >= 0; --i) {
     if (!first) f = fp12_sqr_inl(f);
-    for (int k = 0; k < N; ++k) {
+    int k = 0;
+#if BLS_ML_LINE_PAIR
+    for (; k + 1 < N; k += 2) {
+      E c0, c1, c2, d0, d1, d2;
+      line_dbl(T[k], P[k], c0, c1, c2);
+      line_dbl(T[k + 1], P[k + 1], d0, d1, d2);
+      f = fp12_mul_by_line_pair_inl(f, line_pair_product(c0, c1, c2, d0, d1, d2));
+    }
+#endif
+    for (; k < N; ++k) {
       E c0, c1, c2;
       line_dbl(T[k], P[k], c0, c1, c2);
       f = fp12_mul_by_line_inl(f, c0, c1, c2);
     }
     first = false;
     if ((BLS_X_ABS >> i) & 1) {
-      for (int k = 0; k < N; ++k) {
+      k = 0;
+#if BLS_ML_LINE_PAIR
+      for (; k + 1 < N; k += 2) {
+        E c0, c1, c2, d0, d1, d2;
+        line_add(T[k], Q[k], P[k], c0, c1, c2);
+        line_add(T[k + 1], Q[k + 1], P[k + 1], d0, d1, d2);
+        f = fp12_mul_by_line_pair_inl(f, line_pair_product(c0, c1, c2, d0, d1, d2));
+      }
+#endif
+      for (; k < N; ++k) {
         E c0, c1, c2;
         line_add(T[k], Q[k], P[k], c0, c1, c2);
         f = fp12_mul_by_line_inl(f, c0, c1, c2);
