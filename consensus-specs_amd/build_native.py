@@ -48,13 +48,17 @@ def build_hip(force=False, extra=()):
 SANITIZE_DIR = os.environ.get("BLS381_SANITIZE_DIR", os.path.expanduser("~/.cache/bls381_amd"))
 
 
-def build_hostcheck(force=False, sanitize=False, count_ops=False):
+def build_hostcheck(force=False, sanitize=False, count_ops=False, defines=()):
+    """defines: build-knob variants (e.g. ("BLS_ML_LINE_PAIR=1",)) -- test-only, built out of
+    tree like the sanitized library."""
     os.makedirs(LIB, exist_ok=True)
     name = "libbls381_hostcheck_asan.so" if sanitize else (
         "libbls381_hostcheck_count.so" if count_ops else "libbls381_hostcheck.so")
-    if sanitize:
+    if defines:
+        name = name[:-3] + "_" + "_".join(d.replace("=", "").lower() for d in defines) + ".so"
+    if sanitize or defines:
         os.makedirs(SANITIZE_DIR, exist_ok=True)
-    out = os.path.join(SANITIZE_DIR if sanitize else LIB, name)
+    out = os.path.join(SANITIZE_DIR if (sanitize or defines) else LIB, name)
     src = os.path.join(CSRC, "host_check.cpp")
     deps = [src] + [os.path.join(CSRC, f) for f in HEADERS if f != "bls381_kernels.hpp"]
     if not force and _newer(out, deps):
@@ -65,6 +69,7 @@ def build_hostcheck(force=False, sanitize=False, count_ops=False):
         cmd[2:3] = ["-O0", "-fsanitize=address,undefined", "-fno-omit-frame-pointer"]
     if count_ops:
         cmd[3:3] = ["-DBLS_COUNT_OPS"]
+    cmd[3:3] = ["-D" + d for d in defines]
     _run(cmd)
     return out
 
