@@ -205,7 +205,7 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
 // the batch leaves SIMDs idle (k_final_exp_verdict_q: half the per-item latency, more
 // lane work), on lane pairs above that
 #ifndef BLS_FE_QUAD_MAX_N
-#define BLS_FE_QUAD_MAX_N 16384
+#define BLS_FE_QUAD_MAX_N 49152
 #endif
 int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts) {
   if (n <= BLS_FE_QUAD_MAX_N)
@@ -260,10 +260,12 @@ VerifyWs carve_verify(void* ws, size_t n) {
 // 1: decode_g2 runs on the side stream after decode_g1 (r01k: 1.59-1.61 M ->
 // 1.62 M verifications/s on one box); 0: on the main stream before hash_to_g2
 // bls_verify batches of at most this many items run their Miller loops on lane quads
-// (k_miller_verify_q: 4n lanes <= one wave per SIMD of the 1024), larger ones on lane
-// pairs (k_miller_verify: 13% less work per item, measured at 2^16 items)
+// (k_miller_verify_q), larger ones on lane pairs (k_miller_verify: 13% less work per item).
+// Below ~2^16 items the pair kernels leave SIMDs with one latency-bound wave, so the quads
+// win: r02t, wall ms pair -> quad at 16,385 / 32,768 / 49,152 items: 28.7 -> 18.7 / 20.7 /
+// 27.7; at 65,536 the pairs win (32.4 vs 35.2).  BLS_FE_QUAD_MAX_N follows the same curve.
 #ifndef BLS_ML_QUAD_MAX_N
-#define BLS_ML_QUAD_MAX_N 16384
+#define BLS_ML_QUAD_MAX_N 49152
 #endif
 
 #ifndef BLS_DECODE_G2_SIDE

@@ -204,7 +204,7 @@ def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
     """The golden and torsion bls_verify cases (infinite keys and signatures, bad encodings,
     small-order components, a degenerate Miller loop) tiled to n items, so every Miller /
     final-exponentiation layout sees them: n <= 8192 one quad per Miller pair + the 2-value
-    quad FE, n <= 16384 both pairs on one quad + the quad FE, above that lane pairs (2^18 + 3:
+    quad FE, n <= 49152 both pairs on one quad + the quad FE, above that lane pairs (2^18 + 3:
     launches of several rounds of waves with a ragged last wave).  The tiled verdicts equal the
     untiled batch's, which equal the fixtures' column for the policy."""
     _, gb = golden
@@ -224,7 +224,7 @@ def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
     finally:
         native.set_subgroup_policy("pyecc")
     assert base == [e for _, e in cases]
-    # strict, n > 16384: the signature's G2 test runs on the Miller loop's final point
+    # strict, n > 49152: the signature's G2 test runs on the Miller loop's final point
     assert tiled == [base[i % len(cases)] for i in range(n)]
 
 
