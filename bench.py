@@ -592,7 +592,11 @@ def bench_native_comm(native, args, world, rank, dist, dev):
     else:
         uid = comm.unique_id()
     comm.init(world, rank, uid)
-    out = {"n_gpus": world}
+    # one RCCL in the process: the library reuses the one torch.distributed loaded (if any)
+    import os
+    out = {"n_gpus": world, "rccl": {"library": os.path.realpath(comm.rccl_path()),
+                                     "mapped": comm.loaded_rccl_paths()}}
+    out["rccl"]["single_copy"] = len(out["rccl"]["mapped"]) <= 1
     try:
         k = args.c4_keys * world
         base = native.privtopub_batch(b"".join(j.to_bytes(32, "big") for j in range(1, 65)))

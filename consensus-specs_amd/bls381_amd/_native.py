@@ -32,6 +32,8 @@ _SIGS = {
     "bls381_last_error": (ctypes.c_char_p, []),
     "bls381_set_subgroup_policy": (ctypes.c_int, [ctypes.c_int]),
     "bls381_get_subgroup_policy": (ctypes.c_int, []),
+    "bls381_set_thread_subgroup_policy": (ctypes.c_int, [ctypes.c_int]),
+    "bls381_get_thread_subgroup_policy": (ctypes.c_int, []),
     "bls381_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "bls381_profile_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "bls381_verify": (ctypes.c_int, [_u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]),
@@ -72,6 +74,7 @@ _SIGS = {
                                              _u8p, _u8p]),
     "bls381_final_verify": (ctypes.c_int, [ctypes.c_size_t, _u8p]),
     "bls381_comm_unique_id": (ctypes.c_int, [_u8p]),
+    "bls381_comm_rccl_path": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t]),
     "bls381_comm_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _u8p]),
     "bls381_comm_init_virtual": (ctypes.c_int, [ctypes.c_int]),
     "bls381_comm_size": (ctypes.c_int, []),
@@ -179,6 +182,49 @@ def set_subgroup_policy(name: str) -> None:
 
 def get_subgroup_policy() -> str:
     code = load_library().bls381_get_subgroup_policy()
+    return {v: k for k, v in POLICY.items()}[code]
+
+
+class subgroup_policy_scope:
+    """Context manager: calls queued from this thread inside the block use `name`
+    (bls381_set_thread_subgroup_policy); the process-wide policy is left alone and the
+    thread's previous override is restored on exit."""
+
+    def __init__(self, name: str):
+        if name not in POLICY:
+            raise ValueError("unknown subgroup policy %r (expected one of %s)" % (name, sorted(POLICY)))
+        self.code = POLICY[name]
+
+    def __enter__(self):
+        lib_ = load_library()
+        self.prev = _thread_override.get()
+        check(lib_.bls381_set_thread_subgroup_policy(self.code))
+        _thread_override.set(self.code)
+        return self
+
+    def __exit__(self, *exc):
+        check(load_library().bls381_set_thread_subgroup_policy(self.prev))
+        _thread_override.set(self.prev)
+        return False
+
+
+class _Override:
+    """This thread's override as the library holds it (-1: none); mirrored here so a
+    nested scope can restore it without another call."""
+    _tls = __import__("threading").local()
+
+    def get(self) -> int:
+        return getattr(self._tls, "code", -1)
+
+    def set(self, code: int) -> None:
+        self._tls.code = code
+
+
+_thread_override = _Override()
+
+
+def get_thread_subgroup_policy() -> str:
+    code = load_library().bls381_get_thread_subgroup_policy()
     return {v: k for k, v in POLICY.items()}[code]
 
 

@@ -12,17 +12,28 @@ the same error behaviour as the py_ecc 1.7.0 calls they replace
 * bls_aggregate_* raise ValueError on an invalid point encoding;
 * a domain outside [0, 2^64) raises OverflowError (int.to_bytes).
 
-Messages may have any length up to _native.MSG_MAX (1 MiB; the spec's
-message_hash is Bytes32), and one bls_verify_multiple call may mix lengths (each
-length group becomes a partial Miller product; one final exponentiation decides
-the call).  A longer message raises ValueError instead of returning a verdict.
+Divergences from that contract (each tested in tests/test_abi_and_shim.py):
+* a message longer than _native.MSG_MAX (1 MiB) raises ValueError from bls_verify,
+  bls_verify_multiple and bls_sign, where py_ecc would hash it and return a verdict.
+  The spec's message_hash is Bytes32, so no spec call reaches the limit; raising
+  keeps a verdict from ever being guessed for an input the engine did not hash.
+Messages up to the limit may have any length, and one bls_verify_multiple call may
+mix lengths (each length group becomes a partial Miller product; one final
+exponentiation decides the call).
 
 Two switches mirror behaviour the reference leaves to py_ecc:
 * DOMAIN_BYTEORDER -- how the int domain becomes 8 bytes (SURVEY.md A.2);
-* SUBGROUP_POLICY  -- "pyecc" (default): py_ecc 1.7.0's checks, decoding and
-  on-curve only; "strict": every pubkey / signature must also lie in G1 / G2
-  (specs/bls_signature.md:135-136,143-144).  The verdicts differ only on points
-  with a small-order component (tests/golden/bls_torsion.json has both columns).
+* SUBGROUP_POLICY  -- "pyecc" (default): py_ecc 1.7.0's subgroup behaviour -- no
+  subgroup test, only the on-curve test; "strict": every pubkey / signature must
+  also lie in G1 / G2 (specs/bls_signature.md:135-136,143-144).  The verdicts
+  differ only on points with a small-order component (tests/golden/bls_torsion.json
+  has both columns).  Under either policy *decoding* is the spec's strict codec
+  (bls_signature.md:47-52,58-64: c_flag set, x < q, canonical infinity); py_ecc
+  1.7.0 may accept some non-canonical encodings that this rejects,
+  so "pyecc" names the subgroup behaviour, not the codec.
+  The switch applies to this module's calls only: each verify runs inside a
+  thread-local policy scope (_native.subgroup_policy_scope), so the process-wide
+  policy other front ends read (_native.set_subgroup_policy) is never rewritten.
 """
 from . import _native
 
@@ -88,8 +99,8 @@ def bls_verify(pubkey, message_hash, signature, domain):
     _check_len(message_hash)
     if len(pubkey) != 48 or len(signature) != 96:
         return False
-    _native.set_subgroup_policy(SUBGROUP_POLICY)
-    return _native.verify(pubkey, message_hash, signature, dom8)
+    with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+        return _native.verify(pubkey, message_hash, signature, dom8)
 
 
 @only_with_bls(alt_return=True)
@@ -105,8 +116,8 @@ def bls_verify_multiple(pubkeys, message_hashes, signature, domain):
         _check_len(m)
     if any(len(p) != 48 for p in pks) or len(signature) != 96:
         return False
-    _native.set_subgroup_policy(SUBGROUP_POLICY)
-    return verify_multiple_bytes(pks, msgs, signature, dom8)
+    with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+        return verify_multiple_bytes(pks, msgs, signature, dom8)
 
 
 def verify_multiple_bytes(pks, msgs, signature: bytes, dom8: bytes) -> bool:

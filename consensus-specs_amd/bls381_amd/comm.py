@@ -36,12 +36,18 @@ def unique_id() -> bytes:
 
 
 def exchange_unique_id(rank: int, world: int, addr: str = "127.0.0.1", port: int = 29517,
-                       timeout: float = 120.0) -> bytes:
-    """Rank 0 makes the id and serves it to world - 1 peers; the others fetch it."""
+                       timeout: float = 120.0, make_id=None) -> bytes:
+    """Rank 0 makes the id and serves it to world - 1 peers; the others fetch it.
+
+    make_id: the id factory (default: RCCL's, through bls381_comm_unique_id).  The CPU
+    tests pass a stub, so the rendezvous runs without a GPU (tests/test_sharding.py)."""
+    make_id = make_id or unique_id
     if world == 1:
-        return unique_id()
+        return make_id()
     if rank == 0:
-        uid = unique_id()
+        uid = make_id()
+        if len(uid) != UID_BYTES:
+            raise ValueError("unique id must be %d bytes" % UID_BYTES)
         srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
         srv.bind((addr, port))
@@ -72,6 +78,28 @@ def exchange_unique_id(rank: int, world: int, addr: str = "127.0.0.1", port: int
         if time.time() > deadline:
             raise TimeoutError("no unique id from rank 0 at %s:%d" % (addr, port))
         time.sleep(0.05)
+
+
+def rccl_path() -> str:
+    """The RCCL shared object the library's communicator uses (bls381_comm_rccl_path)."""
+    buf = ctypes.create_string_buffer(4096)
+    _native.check(_native.load_library().bls381_comm_rccl_path(buf, len(buf)))
+    return buf.value.decode()
+
+
+def loaded_rccl_paths() -> List[str]:
+    """Every librccl mapped into this process (from /proc/self/maps), resolved."""
+    import os
+    out = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and "librccl" in os.path.basename(parts[-1]):
+                    out.add(os.path.realpath(parts[-1]))
+    except OSError:
+        pass
+    return sorted(out)
 
 
 def init(world: int, rank: int, uid: bytes) -> None:

@@ -34,8 +34,11 @@ thread_local int t_device = -1;
 
 // Subgroup policy of the verify paths (bls381_set_subgroup_policy); read when a
 // pipeline is queued.  Default: py_ecc 1.7.0's behaviour.
+// A thread may override it for its own calls (bls381_set_thread_subgroup_policy).
 std::atomic<int> g_policy{BLS381_POLICY_PYECC};
-int check_subgroups() { return g_policy.load(std::memory_order_relaxed) == BLS381_POLICY_STRICT ? 1 : 0; }
+thread_local int t_policy = -1;
+int current_policy() { return t_policy >= 0 ? t_policy : g_policy.load(std::memory_order_relaxed); }
+int check_subgroups() { return current_policy() == BLS381_POLICY_STRICT ? 1 : 0; }
 
 // Host memory that an async copy still reads: released once an event
 // recorded after the copy has completed (device-pointer entry points return
@@ -222,8 +225,8 @@ int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* 
 
 // ----------------------------------------------------- verify_batch (C2) --
 struct VerifyWs {
-  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff;
-  uint8_t *pk_st, *sig_st, *f_st;
+  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff, *ml_L;
+  uint8_t *pk_st, *sig_st, *f_st, *ml_st;
 };
 // bls_verify batches of at most this many items run each Miller pair on its own lane
 // quad (k_miller_verify_o, 8 lanes per item: the lowest latency), up to
@@ -239,13 +242,27 @@ struct VerifyWs {
 #endif
 // Fp12 values the Miller stage of a verify batch writes (two per item on the octet path)
 size_t verify_nf(size_t n) { return n <= BLS_ML_OCT_MAX_N ? 2 * n : n; }
+// the split Miller loop (k_ml_lines -> k_ml_accum) of the throughput path runs in chunks of at
+// most this many items; its line products take ML_L_WORDS_PER_ITEM words per item of a chunk
+#ifndef BLS_ML_SPLIT
+#define BLS_ML_SPLIT 1
+#endif
+#ifndef BLS_ML_SPLIT_CHUNK
+#define BLS_ML_SPLIT_CHUNK 65536
+#endif
+bool verify_split(size_t n);
+size_t verify_split_chunk(size_t n) { return verify_split(n) ? std::min<size_t>(n, BLS_ML_SPLIT_CHUNK) : 0; }
 size_t verify_ws_size(size_t n) {
+  const size_t ch = verify_split_chunk(n);
   return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
-         align256(verify_nf(n)) + align256(4 * n) + 1024;
+         align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n) {
   Bump b(ws);
   VerifyWs w;
+  const size_t ch = verify_split_chunk(n);
+  w.ml_L = ch ? b.take<uint32_t>(ML_L_WORDS_PER_ITEM * ch) : nullptr;
+  w.ml_st = ch ? b.take<uint8_t>(ch) : nullptr;
   w.pk_aff = b.take<uint32_t>(2 * FP_LIMBS * n);
   w.sig_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
   w.h_aff = b.take<uint32_t>(4 * FP_LIMBS * n);
@@ -267,6 +284,7 @@ VerifyWs carve_verify(void* ws, size_t n) {
 #ifndef BLS_ML_QUAD_MAX_N
 #define BLS_ML_QUAD_MAX_N 49152
 #endif
+bool verify_split(size_t n) { return BLS_ML_SPLIT && n > BLS_ML_QUAD_MAX_N; }
 
 #ifndef BLS_DECODE_G2_SIDE
 #define BLS_DECODE_G2_SIDE 1
@@ -318,6 +336,18 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("miller_loop_2q", s, dim3(grid_for(4 * n)), b, k_miller_verify_q, n, (const uint32_t*)w.sig_aff,
            (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
            w.f, w.f_st);
+  } else if (verify_split(n)) {
+    // the split Miller loop, in chunks: running points and line products on quads, then the
+    // f accumulation on lane pairs
+    const size_t ch = verify_split_chunk(n);
+    for (size_t i0 = 0; i0 < n; i0 += ch) {
+      const size_t cnt = std::min(ch, n - i0);
+      LAUNCH("miller_lines", s, dim3(grid_for(4 * cnt)), b, k_ml_lines, n, i0, cnt, (const uint32_t*)w.sig_aff,
+             (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+             w.ml_L, w.ml_st, sig_in_loop ? 1 : 0);
+      LAUNCH("miller_accum", s, dim3(grid_for(2 * cnt)), b, k_ml_accum, n, i0, cnt, (const uint32_t*)w.ml_L,
+             (const uint8_t*)w.ml_st, w.f, w.f_st);
+    }
   } else {
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
            (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st,
@@ -1057,6 +1087,14 @@ int bls381_set_subgroup_policy(int policy) {
 }
 
 int bls381_get_subgroup_policy(void) { return g_policy.load(std::memory_order_relaxed); }
+
+int bls381_set_thread_subgroup_policy(int policy) {
+  if (policy != -1 && policy != BLS381_POLICY_PYECC && policy != BLS381_POLICY_STRICT) return BLS381_EARG;
+  t_policy = policy;
+  return 0;
+}
+
+int bls381_get_thread_subgroup_policy(void) { return current_policy(); }
 
 int bls381_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_prof_mu);
@@ -2003,10 +2041,17 @@ RcclApi* rccl_api() {
   static RcclApi api;
   static std::once_flag once;
   std::call_once(once, [] {
-    for (const char* name : {"librccl.so", "librccl.so.1", "/opt/rocm/lib/librccl.so"}) {
-      api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+    // an RCCL the process has already loaded (e.g. PyTorch's torch/lib/librccl.so, soname
+    // librccl.so.1) comes first, so the library and torch.distributed share one RCCL
+    for (const char* name : {"librccl.so.1", "librccl.so"}) {
+      api.h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
       if (api.h) break;
     }
+    if (!api.h)
+      for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so"}) {
+        api.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+        if (api.h) break;
+      }
     if (!api.h) return;
     api.get_unique_id = (decltype(api.get_unique_id))dlsym(api.h, "ncclGetUniqueId");
     api.comm_init_rank = (decltype(api.comm_init_rank))dlsym(api.h, "ncclCommInitRank");
@@ -2081,15 +2126,25 @@ Comm* comm_ctx(int* rc) {
   return &g_comm;
 }
 
+// Every collective exchanges rows through this buffer, allocated when the communicator is
+// made: a rank whose local stage fails still has somewhere to put its zero / error row and
+// takes part in every collective of the call (the other ranks would otherwise wait in RCCL
+// forever).  Row blocks larger than the buffer go through it in pieces.
+constexpr size_t COMM_ROWS_BYTES = 1 << 20;
+
 int comm_rows(Comm* cm, size_t bytes, uint8_t** out) {
   if (cm->rows_cap < bytes) {
-    if (cm->rows) HIPC(hipFree(cm->rows));
-    cm->rows = nullptr;
-    cm->rows_cap = 0;
-    HIPC(hipMalloc(&cm->rows, bytes));
-    cm->rows_cap = bytes;
+    t_err = "collective rows exceed the communicator buffer";
+    *out = nullptr;
+    return BLS381_EARG;
   }
   *out = cm->rows;
+  return 0;
+}
+
+int comm_alloc_rows(Comm* cm) {
+  HIPC(hipMalloc(&cm->rows, COMM_ROWS_BYTES));
+  cm->rows_cap = COMM_ROWS_BYTES;
   return 0;
 }
 
@@ -2098,9 +2153,29 @@ int first_rank(const Comm* cm) { return cm->virt ? 0 : cm->rank; }
 int last_rank(const Comm* cm) { return cm->virt ? cm->nranks - 1 : cm->rank; }
 bool is_root(const Comm* cm) { return cm->virt || cm->rank == 0; }
 
+// runs a rank's local stage of a collective call; exceptions become error codes
+template <class F>
+int local_stage(F&& f) {
+  try {
+    return f();
+  } catch (const std::exception& e) {
+    t_err = e.what();
+    return BLS381_EARG;
+  }
+}
 }  // namespace
 
 extern "C" {
+
+int bls381_comm_rccl_path(char* out, size_t cap) {
+  if (!out || cap == 0) return BLS381_EARG;
+  RcclApi* api = rccl_api();
+  if (!api) return BLS381_ENODEV;
+  Dl_info info;
+  if (!dladdr((void*)api->get_unique_id, &info) || !info.dli_fname) { t_err = "dladdr failed"; return BLS381_EHIP; }
+  std::snprintf(out, cap, "%s", info.dli_fname);
+  return 0;
+}
 
 int bls381_comm_unique_id(uint8_t out[128]) {
   if (!out) return BLS381_EARG;
@@ -2122,10 +2197,15 @@ int bls381_comm_init(int nranks, int rank, const uint8_t uid[128]) {
   if (!api) return BLS381_ENODEV;
   std::lock_guard<std::mutex> lk(g_comm_mu);
   if (g_comm.comm || g_comm.virt) { t_err = "communicator already initialised"; return BLS381_EARG; }
+  if (576 * ((size_t)nranks + 1) + 1024 > COMM_ROWS_BYTES) { t_err = "too many ranks"; return BLS381_EARG; }
+  Comm fresh;
+  if ((rc = comm_alloc_rows(&fresh))) return rc;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof(id));
   ncclComm_t comm;
-  NCCLC(api, api->comm_init_rank(&comm, nranks, id, rank));
+  ncclResult_t nr = api->comm_init_rank(&comm, nranks, id, rank);
+  if (nr != ncclSuccess) { (void)hipFree(fresh.rows); return nccl_fail(api, "ncclCommInitRank", nr); }
+  g_comm = fresh;
   g_comm.comm = comm;
   g_comm.nranks = nranks;
   g_comm.rank = rank;
@@ -2140,6 +2220,10 @@ int bls381_comm_init_virtual(int nranks) {
   if (!c) return rc;
   std::lock_guard<std::mutex> lk(g_comm_mu);
   if (g_comm.comm || g_comm.virt) { t_err = "communicator already initialised"; return BLS381_EARG; }
+  if (576 * ((size_t)nranks + 1) + 1024 > COMM_ROWS_BYTES) { t_err = "too many ranks"; return BLS381_EARG; }
+  Comm fresh;
+  if ((rc = comm_alloc_rows(&fresh))) return rc;
+  g_comm = fresh;
   g_comm.virt = true;
   g_comm.nranks = nranks;
   g_comm.rank = 0;
@@ -2147,8 +2231,14 @@ int bls381_comm_init_virtual(int nranks) {
   return 0;
 }
 
-int bls381_comm_size(void) { return (g_comm.comm || g_comm.virt) ? g_comm.nranks : 0; }
-int bls381_comm_rank(void) { return (g_comm.comm || g_comm.virt) ? g_comm.rank : -1; }
+int bls381_comm_size(void) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  return (g_comm.comm || g_comm.virt) ? g_comm.nranks : 0;
+}
+int bls381_comm_rank(void) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  return (g_comm.comm || g_comm.virt) ? g_comm.rank : -1;
+}
 
 void bls381_comm_destroy(void) {
   std::lock_guard<std::mutex> lk(g_comm_mu);
@@ -2163,12 +2253,19 @@ void bls381_comm_destroy(void) {
   g_comm = Comm();
 }
 
+// Collective calls: every rank issues the same collectives in the same order whatever happens
+// locally.  A rank whose local stage fails (a plan, a workspace or a HIP error) contributes a
+// zero row -- never an honest partial -- so the call's verdict is False / its aggregate is
+// flagged, joins every collective, and returns its own error code afterwards.  g_comm_mu is
+// held for the whole call (comm state, the row buffer and the collective sequence).
+
 int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* msgs, size_t msg_len,
-                                   const uint8_t sig[96], const uint8_t dom8[8]) try {
+                                   const uint8_t sig[96], const uint8_t dom8[8]) {
   if ((n && (!pks || (!msgs && msg_len))) || !sig || !dom8 || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
+  std::lock_guard<std::mutex> clk(g_comm_mu);
   Comm* cm = comm_ctx(&rc);
   if (!cm) return rc;
   RcclApi* api = cm->virt ? nullptr : rccl_api();
@@ -2177,76 +2274,94 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
   const size_t R = (size_t)cm->nranks;
   hipStream_t s = c->stream;
   uint8_t* d_rows;
-  if ((rc = comm_rows(cm, 576 * R + 576, &d_rows))) return rc;
-  // distinct message k (first-appearance order) -> rank k mod nranks: a message's
-  // pubkey group never straddles two ranks (bls381_amd/sharding.py partition_messages)
-  std::unordered_map<std::string, uint32_t> order;
-  std::vector<uint32_t> owner(n);
-  for (size_t i = 0; i < n; ++i) {
-    std::string key((const char*)msgs + msg_len * i, msg_len);
-    auto it = order.find(key);
-    if (it == order.end()) it = order.emplace(key, (uint32_t)order.size()).first;
-    owner[i] = it->second % (uint32_t)R;
-  }
-  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
-    std::vector<uint8_t> my_pks, my_msgs;
+  if ((rc = comm_rows(cm, 576 * R + 576 + 64, &d_rows))) return rc;   // fits by construction (init)
+  uint8_t* d_v = d_rows + 576 * R + 576;
+  // local stage: this rank's row(s); on failure the row is zero (verdict False on rank 0)
+  int local = local_stage([&]() -> int {
+    // distinct message k (first-appearance order) -> rank k mod nranks: a message's
+    // pubkey group never straddles two ranks (bls381_amd/sharding.py partition_messages)
+    std::unordered_map<std::string, uint32_t> order;
+    std::vector<uint32_t> owner(n);
     for (size_t i = 0; i < n; ++i) {
-      if ((int)owner[i] != r) continue;
-      my_pks.insert(my_pks.end(), pks + 48 * i, pks + 48 * (i + 1));
-      my_msgs.insert(my_msgs.end(), msgs + msg_len * i, msgs + msg_len * (i + 1));
+      std::string key((const char*)msgs + msg_len * i, msg_len);
+      auto it = order.find(key);
+      if (it == order.end()) it = order.emplace(key, (uint32_t)order.size()).first;
+      owner[i] = it->second % (uint32_t)R;
     }
-    const uint32_t off[2] = {0, (uint32_t)(my_pks.size() / 48)};
-    const int with_sig = r == 0 ? 1 : 0;
-    Bump b(nullptr, 0);
-    uint32_t* f;
-    uint8_t* st;
-    if ((rc = vm_host(c, 1, off, my_pks.data(), my_msgs.data(), msg_len, sig, dom8, &with_sig, b, &f, &st)))
-      return rc;
-    // this rank's row (576 B, zero when a member is invalid): in place when virtual
-    uint8_t* row = cm->virt ? d_rows + 576 * (size_t)r : d_rows + 576 * R;
-    LAUNCH("fp12_row", s, dim3(1), dim3(KBLOCK), k_fp12_row, (const uint32_t*)f, (const uint8_t*)st, row);
-    HIPC(hipStreamSynchronize(s));   // the next rank's plan reuses the workspace
+    int lrc = 0;
+    for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
+      std::vector<uint8_t> my_pks, my_msgs;
+      for (size_t i = 0; i < n; ++i) {
+        if ((int)owner[i] != r) continue;
+        my_pks.insert(my_pks.end(), pks + 48 * i, pks + 48 * (i + 1));
+        my_msgs.insert(my_msgs.end(), msgs + msg_len * i, msgs + msg_len * (i + 1));
+      }
+      const uint32_t off[2] = {0, (uint32_t)(my_pks.size() / 48)};
+      const int with_sig = r == 0 ? 1 : 0;
+      Bump b(nullptr, 0);
+      uint32_t* f;
+      uint8_t* st;
+      if ((lrc = vm_host(c, 1, off, my_pks.data(), my_msgs.data(), msg_len, sig, dom8, &with_sig, b, &f, &st)))
+        return lrc;
+      // this rank's row (576 B, zero when a member is invalid): in place when virtual
+      uint8_t* row = cm->virt ? d_rows + 576 * (size_t)r : d_rows + 576 * R;
+      LAUNCH("fp12_row", s, dim3(1), dim3(KBLOCK), k_fp12_row, (const uint32_t*)f, (const uint8_t*)st, row);
+      HIPC(hipStreamSynchronize(s));   // the next rank's plan reuses the workspace
+    }
+    return 0;
+  });
+  if (local) {
+    (void)hipStreamSynchronize(s);
+    if (cm->virt) return local;
+    if (hipMemset(d_rows + 576 * R, 0, 576) != hipSuccess) return local;   // row unusable: RCCL cannot help
   }
   if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 576 * R, d_rows, 576, ncclUint8, cm->comm, s));
-  if ((rc = ensure_ws(c, 12 * FPW * R * 4 + 4 * R + 65536))) return rc;
-  Bump b(c->ws, c->ws_cap);
-  uint8_t* d_v = b.take<uint8_t>(1);
-  if (is_root(cm)) {   // one final exponentiation, on rank 0
-    uint32_t* g = b.take<uint32_t>(12 * FP_LIMBS * R);
-    uint8_t* gst = b.take<uint8_t>(R);
-    HIPC(hipMemsetAsync(gst, ST_OK, R, s));
-    LAUNCH("fp12_from_bytes", s, dim3(grid_for(2 * R)), dim3(KBLOCK), k_fp12_from_bytes, R, (const uint8_t*)d_rows, g);
-    auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products({0u, (uint32_t)R}));
-    size_t n_in = R;
-    for (const auto& chunks : *passes) {
-      agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
-      uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
-      uint8_t* nst = b.take<uint8_t>(chunks.size());
-      HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
-      LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), dim3(KBLOCK), k_fp12_chunk_product, chunks.size(),
-             (const agg_chunk*)d_ch, (const uint32_t*)g, n_in, (const uint8_t*)gst, nf, nst);
-      g = nf;
-      gst = nst;
-      n_in = chunks.size();
+  if (is_root(cm)) {   // one final exponentiation, on rank 0 (verdict 0 if it cannot run)
+    HIPC(hipMemsetAsync(d_v, 0, 1, s));
+    const int root = local_stage([&]() -> int {
+      int lrc;
+      if ((lrc = ensure_ws(c, 12 * FPW * R * 4 + 4 * R + 65536))) return lrc;
+      Bump b(c->ws, c->ws_cap);
+      uint32_t* g = b.take<uint32_t>(12 * FP_LIMBS * R);
+      uint8_t* gst = b.take<uint8_t>(R);
+      HIPC(hipMemsetAsync(gst, ST_OK, R, s));
+      LAUNCH("fp12_from_bytes", s, dim3(grid_for(2 * R)), dim3(KBLOCK), k_fp12_from_bytes, R, (const uint8_t*)d_rows, g);
+      auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products({0u, (uint32_t)R}));
+      size_t n_in = R;
+      for (const auto& chunks : *passes) {
+        agg_chunk* d_ch = b.take<agg_chunk>(chunks.size());
+        uint32_t* nf = b.take<uint32_t>(12 * FP_LIMBS * chunks.size());
+        uint8_t* nst = b.take<uint8_t>(chunks.size());
+        HIPC(hipMemcpyAsync(d_ch, chunks.data(), chunks.size() * sizeof(agg_chunk), hipMemcpyHostToDevice, s));
+        LAUNCH("fp12_product", s, dim3(grid_for(2 * chunks.size())), dim3(KBLOCK), k_fp12_chunk_product,
+               chunks.size(), (const agg_chunk*)d_ch, (const uint32_t*)g, n_in, (const uint8_t*)gst, nf, nst);
+        g = nf;
+        gst = nst;
+        n_in = chunks.size();
+      }
+      LAUNCH_FE(s, (size_t)1, g, gst, d_v);
+      return keep_until_done(c, s, passes);
+    });
+    if (root) {
+      (void)hipStreamSynchronize(s);
+      (void)hipMemset(d_v, 0, 1);
+      if (!local) local = root;
     }
-    LAUNCH_FE(s, (size_t)1, g, gst, d_v);
-    if ((rc = keep_until_done(c, s, passes))) return rc;
   }
   if (!cm->virt) NCCLC(api, api->broadcast(d_v, d_v, 1, ncclUint8, 0, cm->comm, s));
   uint8_t v = 0;
   HIPC(hipMemcpyAsync(&v, d_v, 1, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
+  if (local) return local;
   return v ? 1 : 0;
-} catch (const std::exception& e) {
-  t_err = e.what();
-  return BLS381_EARG;
 }
 
-int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]) try {
+int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]) {
   if (!out || (n && !pks)) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
+  std::lock_guard<std::mutex> clk(g_comm_mu);
   Comm* cm = comm_ctx(&rc);
   if (!cm) return rc;
   RcclApi* api = cm->virt ? nullptr : rccl_api();
@@ -2255,33 +2370,54 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
   std::lock_guard<std::mutex> lk(c->mu);
   hipStream_t s = c->stream;
   uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
-  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;
+  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;   // fits by construction (init)
   uint8_t* d_sum = d_rows + 48 * R + 48;
   int32_t* d_st = (int32_t*)(d_sum + 64);
   // contiguous ranges, sizes differing by at most one (sharding.shard_range)
   const size_t base = n / R, extra = n % R;
+  int local = 0;
   for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
     const size_t rr = (size_t)r;
-    const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
-    const uint32_t off1[2] = {0, (uint32_t)cnt};
-    const size_t ws1 = agg_ws_bytes(0, 1, off1);
-    if ((rc = ensure_ws(c, align256(48 * cnt + 1) + ws1 + 8192))) return rc;
-    Bump b(c->ws, c->ws_cap);
-    uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
-    void* w1 = b.take<uint8_t>(ws1);
-    if (cnt) HIPC(hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s));
     uint8_t* part = cm->virt ? d_rows + 48 * rr : d_rows + 48 * R;
-    if ((rc = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s))) return rc;
-    // an invalid encoding anywhere: this partial becomes 48 zero bytes, itself invalid
-    LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
-    HIPC(hipStreamSynchronize(s));   // the host slice and the workspace are reused
+    const int lrc = local_stage([&]() -> int {
+      const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
+      const uint32_t off1[2] = {0, (uint32_t)cnt};
+      const size_t ws1 = agg_ws_bytes(0, 1, off1);
+      int e;
+      if ((e = ensure_ws(c, align256(48 * cnt + 1) + ws1 + 8192))) return e;
+      Bump b(c->ws, c->ws_cap);
+      uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
+      void* w1 = b.take<uint8_t>(ws1);
+      if (cnt) HIPC(hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s));
+      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s))) return e;
+      // an invalid encoding anywhere: this partial becomes 48 zero bytes, itself invalid
+      LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
+      HIPC(hipStreamSynchronize(s));   // the host slice and the workspace are reused
+      return 0;
+    });
+    if (lrc) {
+      (void)hipStreamSynchronize(s);
+      (void)hipMemset(part, 0, 48);   // 48 zero bytes: not an encoding, the sum is flagged
+      if (!local) local = lrc;
+    }
   }
+  if (local && cm->virt) return local;
   if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 48 * R, d_rows, 48, ncclUint8, cm->comm, s));
   if (is_root(cm)) {   // the partials are compressed points: decode + sum them on rank 0
-    const uint32_t offR[2] = {0, (uint32_t)R};
-    const size_t wsR = agg_ws_bytes(0, 1, offR);
-    if ((rc = ensure_ws(c, wsR + 4096))) return rc;
-    if ((rc = agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s))) return rc;
+    const int root = local_stage([&]() -> int {
+      const uint32_t offR[2] = {0, (uint32_t)R};
+      const size_t wsR = agg_ws_bytes(0, 1, offR);
+      int e;
+      if ((e = ensure_ws(c, wsR + 4096))) return e;
+      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s);
+    });
+    if (root) {
+      (void)hipStreamSynchronize(s);
+      const int32_t err = BLS381_EHIP;
+      (void)hipMemset(d_sum, 0, 48);
+      (void)hipMemcpy(d_st + 1, &err, 4, hipMemcpyHostToDevice);
+      if (!local) local = root;
+    }
   }
   if (!cm->virt) {
     NCCLC(api, api->broadcast(d_sum, d_sum, 48, ncclUint8, 0, cm->comm, s));
@@ -2291,20 +2427,18 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
   HIPC(hipMemcpyAsync(out, d_sum, 48, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(&st, d_st + 1, 4, hipMemcpyDeviceToHost, s));
   HIPC(hipStreamSynchronize(s));
-  return st;
-} catch (const std::exception& e) {
-  t_err = e.what();
-  return BLS381_EARG;
+  return local ? local : st;
 }
 
 int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
                                          const uint8_t* msgs, size_t msg_len, const uint8_t* sigs,
-                                         const uint8_t* dom8s, uint8_t* verdicts) try {
+                                         const uint8_t* dom8s, uint8_t* verdicts) {
   if (!call_off || !sigs || !dom8s || !verdicts || msg_len > BLS381_MSG_MAX) return BLS381_EARG;
   if (call_off[n_calls] && (!pks || (!msgs && msg_len))) return BLS381_EARG;
   int rc = 0;
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
+  std::lock_guard<std::mutex> clk(g_comm_mu);
   Comm* cm = comm_ctx(&rc);
   if (!cm) return rc;
   RcclApi* api = cm->virt ? nullptr : rccl_api();
@@ -2313,36 +2447,44 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
   const size_t base = n_calls / R, extra = n_calls % R, width = base + (extra ? 1 : 0);
   if (width == 0) return 0;
   std::vector<uint8_t> rows(width * R, 0);
+  int local = 0;
   for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
     const size_t rr = (size_t)r;
     const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
     if (!cnt) continue;
-    std::vector<uint32_t> off(cnt + 1);
-    for (size_t k = 0; k <= cnt; ++k) off[k] = call_off[lo + k] - call_off[lo];
-    const size_t k0 = call_off[lo];
-    if ((rc = bls381_verify_multiple_batch(cnt, off.data(), pks ? pks + 48 * k0 : nullptr,
-                                           msgs ? msgs + msg_len * k0 : nullptr, msg_len, sigs + 96 * lo,
-                                           dom8s + 8 * lo, rows.data() + width * rr)))
-      return rc;
+    const int lrc = local_stage([&]() -> int {
+      std::vector<uint32_t> off(cnt + 1);
+      for (size_t k = 0; k <= cnt; ++k) off[k] = call_off[lo + k] - call_off[lo];
+      const size_t k0 = call_off[lo];
+      return bls381_verify_multiple_batch(cnt, off.data(), pks ? pks + 48 * k0 : nullptr,
+                                          msgs ? msgs + msg_len * k0 : nullptr, msg_len, sigs + 96 * lo,
+                                          dom8s + 8 * lo, rows.data() + width * rr);
+    });
+    if (lrc) {   // this rank's calls count as False for the others; it returns the error
+      std::fill(rows.begin() + width * rr, rows.begin() + width * (rr + 1), (uint8_t)0);
+      if (!local) local = lrc;
+    }
   }
-  if (!cm->virt) {   // all-gather the verdict rows (each rank filled its own)
+  if (!cm->virt) {   // all-gather the verdict rows (each rank filled its own), through the comm buffer
     std::lock_guard<std::mutex> lk(c->mu);
     hipStream_t s = c->stream;
     uint8_t* d_rows;
-    if ((rc = comm_rows(cm, width * (R + 1), &d_rows))) return rc;
-    HIPC(hipMemcpyAsync(d_rows + width * R, rows.data() + width * (size_t)cm->rank, width, hipMemcpyHostToDevice, s));
-    NCCLC(api, api->all_gather(d_rows + width * R, d_rows, width, ncclUint8, cm->comm, s));
-    HIPC(hipMemcpyAsync(rows.data(), d_rows, width * R, hipMemcpyDeviceToHost, s));
-    HIPC(hipStreamSynchronize(s));
+    const size_t piece = std::min(width, COMM_ROWS_BYTES / (R + 1));
+    if ((rc = comm_rows(cm, piece * (R + 1), &d_rows))) return rc;   // fits by construction
+    for (size_t at = 0; at < width; at += piece) {   // same piece count on every rank (width is)
+      const size_t w = std::min(piece, width - at);
+      HIPC(hipMemcpyAsync(d_rows + piece * R, rows.data() + width * (size_t)cm->rank + at, w, hipMemcpyHostToDevice, s));
+      NCCLC(api, api->all_gather(d_rows + piece * R, d_rows, w, ncclUint8, cm->comm, s));
+      for (size_t q = 0; q < R; ++q)
+        HIPC(hipMemcpyAsync(rows.data() + width * q + at, d_rows + w * q, w, hipMemcpyDeviceToHost, s));
+      HIPC(hipStreamSynchronize(s));
+    }
   }
   for (size_t q = 0; q < R; ++q) {
     const size_t qlo = q * base + (q < extra ? q : extra), qcnt = base + (q < extra ? 1 : 0);
     std::memcpy(verdicts + qlo, rows.data() + width * q, qcnt);
   }
-  return 0;
-} catch (const std::exception& e) {
-  t_err = e.what();
-  return BLS381_EARG;
+  return local;
 }
 
 }  // extern "C"

@@ -249,6 +249,161 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify(s
   if (lead) st_out[i] = bad ? ST_BAD : ST_OK;
 }
 
+// ----------------------------------------- split Miller loop (throughput path) --
+// The two-pair Miller loop of k_miller_verify in two kernels, so that neither holds the
+// other's state (DESIGN.md §6 "Split Miller loop"):
+//   k_ml_lines   one item per lane quad.  The lo half runs the running point of the pair
+//                (sig, -[c]g1), the hi half that of (BP(H0), pk).  At each of the 68 Miller
+//                steps the two halves' lines l (lo) and l' (hi) are multiplied on the quad
+//                into L = l l' (6 Fp2 products, 3 per half) and L is written to HBM.
+//   k_ml_accum   one item per lane pair: f <- f^2 L (doubling steps) or f L (addition
+//                steps), f^2 and the sparse product f L (17 Fp2 products) with f in registers.
+// Per doubling step this is 12 + 17 + 6 = 35 Fp2 products of f arithmetic instead of the
+// 12 + 2 x 13 = 38 of miller_loop_n<2>, and the doubling kernel's live set is one running
+// point per lane instead of f plus two points.  The product is the same field element.
+// L layout (per item i of a chunk of cnt items, step j, Fp2 component c, this lane's
+// coefficient p): limb k at L[((j * ML_LC + c) * 14 + k) * 2 cnt + 2 i + p], c = 0..2 the
+// w^0 half (L00, L01, L02), c = 3..4 (L11, L12) -- L10 is always zero.
+constexpr int ML_STEPS = 68;   // 63 doubling + 5 addition steps over |x|
+constexpr int ML_LC = 5;
+constexpr size_t ML_L_WORDS_PER_ITEM = (size_t)ML_STEPS * ML_LC * FP_LIMBS * 2;
+enum : uint8_t { ML_ST_ONE = 4 };   // both pairs infinite: the item's Miller value is 1
+
+// L = l l' of the lo half's line l = x (c0, c1, c2) and the hi half's l' (d0, d1, d2), on a quad:
+//   t0 = c0 d0, t1 = c1 d1, s = c2 d2 (lo: t0, t1, (c0+c1)(d0+d1); hi: s, (c0+c2)(d0+d2), (c1+c2)(d1+d2))
+//   lo: L00 = t0 + xi s, L01 = m01 - t0 - t1, L02 = t1;   hi: L11 = m02 - t0 - s, L12 = m12 - t1 - s
+// (line_pair_product in bls381_pairing.hpp, with the products split over the halves).  Each
+// lane's x is its own half's line; on return lo holds (L00, L01, L02), hi (L11, L12, -).
+__device__ __forceinline__ void quad_line_pair(const fp2p_t& x0, const fp2p_t& x1, const fp2p_t& x2, fp2p_t& o0,
+                                               fp2p_t& o1, fp2p_t& o2) {
+  const bool hi = qd_hi();
+  const fp2p_t y0 = qd_swap(x0), y1 = qd_swap(x1), y2 = qd_swap(x2);
+  // products are symmetric in (c, d), so each half pairs its own line with the other's
+  const fp2p_t p0 = fp2_mul(qd_sel(hi, x2, x0), qd_sel(hi, y2, y0));                   // t0 | s
+  const fp2p_t p1 = fp2_mul(qd_sel(hi, fp2_add_lazy(x0, x2), x1), qd_sel(hi, fp2_add_lazy(y0, y2), y1));   // t1 | m02
+  const fp2p_t p2 = fp2_mul(qd_sel(hi, fp2_add_lazy(x1, x2), fp2_add_lazy(x0, x1)),
+                            qd_sel(hi, fp2_add_lazy(y1, y2), fp2_add_lazy(y0, y1)));   // m01 | m12
+  const fp2p_t q0 = qd_swap(p0), q1 = qd_swap(p1);   // lo: s, m02;  hi: t0, t1
+  // lo: L00 = p0 + xi q0, L01 = p2 - p0 - p1, L02 = p1;  hi: L11 = p1 - q0 - p0, L12 = p2 - q1 - p0
+  o0 = qd_sel(hi, fp2_sub2(p1, q0, p0), fp2_add_mul_xi(p0, q0));
+  o1 = fp2_sub2(p2, qd_sel(hi, q1, p0), qd_sel(hi, p0, p1));
+  o2 = p1;
+}
+
+__device__ __forceinline__ void ml_store_L(uint32_t* __restrict__ L, size_t cnt, size_t i, int j, bool hi,
+                                           const fp2p_t& o0, const fp2p_t& o1, const fp2p_t& o2) {
+  const size_t col = 2 * i + (pr_odd() ? 1 : 0);
+  const int c = j * ML_LC + (hi ? 3 : 0);
+  soa_st(L, 2 * cnt, col, c + 0, o0.v);
+  soa_st(L, 2 * cnt, col, c + 1, o1.v);
+  if (!hi) soa_st(L, 2 * cnt, col, c + 2, o2.v);
+}
+
+// the 68 steps of one half's running point, with the quad's line products written to L
+__device__ __noinline__ void ml_lines_run(const aff_t<fp2p_t>& Q, const g1_line_pre& pre, bool active,
+                                         uint32_t* __restrict__ L, size_t cnt, size_t li, g2_proj<fp2p_t>& T) {
+  const bool hi = qd_hi();
+  const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
+  T.x = Q.x; T.y = Q.y; T.z = one;
+  int j = 0;
+  for (int b = 62; b >= 0; --b) {
+    fp2p_t c0, c1, c2, o0, o1, o2;
+    line_dbl(T, pre, c0, c1, c2);
+    quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
+    ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
+    if ((BLS_X_ABS >> b) & 1) {
+      line_add(T, Q, pre, c0, c1, c2);
+      quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
+      ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
+    }
+  }
+}
+
+// items i0 .. i0 + cnt - 1 of the batch (SoA inputs of n items); L and st_out are chunk-local
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t n, size_t i0, size_t cnt,
+                                                    const uint32_t* __restrict__ sig_aff,
+                                                    const uint8_t* __restrict__ sig_st,
+                                                    const uint32_t* __restrict__ pk_aff,
+                                                    const uint8_t* __restrict__ pk_st,
+                                                    const uint32_t* __restrict__ h_aff,
+                                                    uint32_t* __restrict__ L, uint8_t* __restrict__ st_out,
+                                                    int sig_check) {
+  const size_t li = item_index<4>();
+  if (li >= cnt) return;
+  const size_t i = i0 + li;
+  const bool hi = qd_hi();
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const size_t lp = 2 * i + (pr_odd() ? 1 : 0);
+  const uint8_t ss = sig_st[i], ps = pk_st[i];
+  if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[li] = ST_BAD; return; }
+  const bool sig_ok = ss == ST_OK, pk_ok = ps == ST_OK;
+  if (!sig_ok && !pk_ok) { if (lead) st_out[li] = ML_ST_ONE; return; }
+  // an inactive half (infinite point) runs the other half's pair with its lines masked to 1
+  const bool active = hi ? pk_ok : sig_ok;
+  const bool use_pk = hi ? pk_ok : !sig_ok;
+  const uint32_t* qsrc = use_pk ? h_aff : sig_aff;
+  aff_t<fp2p_t> Q;
+  Q.x = pr_make(soa_ld(qsrc, 2 * n, lp, 0));
+  Q.y = pr_make(soa_ld(qsrc, 2 * n, lp, 1));
+  aff_t<fp_t> P;
+  if (use_pk) {
+    P = soa_ld_g1(pk_aff, n, i);
+  } else {
+    P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
+  }
+  const g1_line_pre pre = g1_prepare(P);
+  g2_proj<fp2p_t> T;
+  ml_lines_run(Q, pre, active, L, cnt, li, T);
+  // py_ecc's zero pairing value for a degenerate loop; the strict policy's G2 test of the
+  // signature on the lo half's final point (psi(sig) == -[|x|] sig)
+  bool bad = active && fp2_is_zero(T.z);
+  if (sig_check && !hi && sig_ok && !bad) bad = !g2_psi_matches_neg(Q, T);
+  bad = !qd_all(!bad);
+  if (lead) st_out[li] = bad ? ST_BAD : ST_OK;
+}
+
+__device__ __forceinline__ fp12p_t ml_load_L(const uint32_t* __restrict__ L, size_t cnt, size_t i, int j) {
+  const size_t col = 2 * i + (pr_odd() ? 1 : 0);
+  const int c = j * ML_LC;
+  fp12p_t r;
+  r.c0.c0 = pr_make(soa_ld(L, 2 * cnt, col, c + 0));
+  r.c0.c1 = pr_make(soa_ld(L, 2 * cnt, col, c + 1));
+  r.c0.c2 = pr_make(soa_ld(L, 2 * cnt, col, c + 2));
+  r.c1.c0 = e2_zero<fp2p_t>();
+  r.c1.c1 = pr_make(soa_ld(L, 2 * cnt, col, c + 3));
+  r.c1.c2 = pr_make(soa_ld(L, 2 * cnt, col, c + 4));
+  return r;
+}
+
+// f = conj(prod_j L_j^(2^(later doublings))) for items i0 .. i0 + cnt - 1; writes f (SoA over n
+// items, the layout k_final_exp_verdict reads) and the item status
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t n, size_t i0, size_t cnt,
+                                                    const uint32_t* __restrict__ L,
+                                                    const uint8_t* __restrict__ st_in,
+                                                    uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  const size_t li = item_index<2>();
+  if (li >= cnt) return;
+  const size_t i = i0 + li;
+  const bool lead = !pr_odd();
+  const uint8_t s = st_in[li];
+  if (s == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
+  fp12p_t f;
+  if (s == ML_ST_ONE) {
+    f = fp12_one<fp2p_t>();
+  } else {
+    f = ml_load_L(L, cnt, li, 0);
+    int j = 1;
+    if ((BLS_X_ABS >> 62) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
+    for (int b = 61; b >= 0; --b) {
+      f = fp12_mul_by_line_pair_inl(fp12_sqr_inl(f), ml_load_L(L, cnt, li, j++));
+      if ((BLS_X_ABS >> b) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
+    }
+    f = fp12_conj(f);
+  }
+  soa_st12(f_out, n, i, f);
+  if (lead) st_out[i] = ST_OK;
+}
+
 // The same verify on a lane quad (bls381_quad.hpp): the lo half runs the pair
 // (sig, -g1), the hi half (H(m), pk), side by side; a single finite pair runs on
 // lo with the hi half idle.  f is stored in the layout of k_miller_verify (each

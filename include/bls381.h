@@ -62,10 +62,16 @@ void bls381_shutdown(void);
 /* Last HIP error string of this thread (static storage). */
 const char* bls381_last_error(void);
 /* Process-wide subgroup policy (BLS381_POLICY_*), read when a call is queued.
- * The Python shim sets it from bls.SUBGROUP_POLICY before each verify.
  * Returns 0, or BLS381_EARG for an unknown policy.  Needs no device. */
 int bls381_set_subgroup_policy(int policy);
 int bls381_get_subgroup_policy(void);
+/* Policy override for calls queued from the calling thread only (-1 clears it and the
+ * thread follows the process-wide policy again).  The Python shim (bls.py) scopes each
+ * verify with its module switch this way, so it neither rewrites the process-wide policy
+ * that other front ends read nor races with other threads.  Returns 0 or BLS381_EARG. */
+int bls381_set_thread_subgroup_policy(int policy);
+/* The policy calls queued from this thread use (the override if set). */
+int bls381_get_thread_subgroup_policy(void);
 /* Kernel-time accounting (HIP events on the launch stream) for bench.py. */
 int bls381_profile_enable(int on);
 int bls381_profile_read(char* json_out, size_t cap);
@@ -224,6 +230,9 @@ int bls381_final_verify(size_t k, const uint8_t* parts576);
  * device it selected with bls381_init.  No PyTorch anywhere. */
 int bls381_comm_unique_id(uint8_t out[128]);
 int bls381_comm_init(int nranks, int rank, const uint8_t uid[128]);
+/* Path of the RCCL shared object the library uses (an RCCL the process already loaded,
+ * e.g. PyTorch's, is preferred over a fresh dlopen; needs no device).  0, or ENODEV. */
+int bls381_comm_rccl_path(char* out, size_t cap);
 /* One process plays all nranks ranks on its own GPU: the same partition and
  * rank-0 combination, the all-gather a device copy (RCCL refuses two ranks on
  * one GPU; this is how a one-GPU box runs the N-rank protocol). */

@@ -99,3 +99,65 @@ def test_registry_shim_hook_is_opt_in():
     assert bls._pubkey_registry is None
     bls.use_pubkey_registry(None)
     assert bls._pubkey_registry is None
+
+
+def test_message_longer_than_limit_raises():
+    """The one divergence from py_ecc's bool-only verify contract (bls.py header): a message
+    over _native.MSG_MAX raises ValueError before any engine call."""
+    from bls381_amd import _native, bls
+    big = b"\x00" * (_native.MSG_MAX + 1)
+    with pytest.raises(ValueError):
+        bls.bls_verify(b"\x00" * 48, big, b"\x00" * 96, 0)
+    with pytest.raises(ValueError):
+        bls.bls_verify_multiple([b"\x00" * 48], [big], b"\x00" * 96, 0)
+    with pytest.raises(ValueError):
+        bls.bls_sign(big, 1, 0)
+
+
+def test_thread_policy_override_is_per_thread():
+    """bls381_set_thread_subgroup_policy: a thread's override never changes the
+    process-wide policy other threads and front ends read, and -1 clears it."""
+    import threading
+    from bls381_amd import _native
+    _native.set_subgroup_policy("strict")
+    try:
+        seen = {}
+        with _native.subgroup_policy_scope("pyecc"):
+            assert _native.get_thread_subgroup_policy() == "pyecc"
+            assert _native.get_subgroup_policy() == "strict"
+            t = threading.Thread(target=lambda: seen.setdefault("other", _native.get_thread_subgroup_policy()))
+            t.start()
+            t.join()
+            with _native.subgroup_policy_scope("strict"):
+                assert _native.get_thread_subgroup_policy() == "strict"
+            assert _native.get_thread_subgroup_policy() == "pyecc"   # nested scope restored
+        assert seen["other"] == "strict"
+        assert _native.get_thread_subgroup_policy() == "strict"      # override cleared
+        L = _native.load_library()
+        assert L.bls381_set_thread_subgroup_policy(7) == _native.EARG
+    finally:
+        _native.set_subgroup_policy("pyecc")
+
+
+def test_shim_does_not_rewrite_process_policy():
+    """bls.bls_verify scopes its policy to the call: a process-wide 'strict' set by another
+    front end survives a shim call (here one that stops before the device: a wrong length)."""
+    from bls381_amd import _native, bls
+    _native.set_subgroup_policy("strict")
+    try:
+        assert bls.bls_verify(b"\x00" * 47, b"\x00" * 32, b"\x00" * 96, 0) is False
+        assert _native.get_subgroup_policy() == "strict"
+    finally:
+        _native.set_subgroup_policy("pyecc")
+
+
+def test_rccl_path_resolves_without_a_device():
+    """bls381_comm_rccl_path: the RCCL the communicator would use (dlopen only, no device);
+    bench.py records it next to the librccl objects mapped in the process."""
+    from bls381_amd import comm
+    try:
+        p = comm.rccl_path()
+    except Exception as e:   # an image without RCCL: the native multi-GPU path is unavailable
+        pytest.skip("RCCL not loadable: %s" % e)
+    assert "rccl" in os.path.basename(p)
+    assert os.path.realpath(p) in comm.loaded_rccl_paths()

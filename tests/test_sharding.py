@@ -206,3 +206,45 @@ def test_sharded_verify_multiple_batch_gloo_world2(case):
     want = [True, True, False, False, False, True]
     res = _run(calls, kind="batch")
     assert res == {0: want, 1: want}
+
+
+# ---------------------------------------- native communicator rendezvous (comm.py)
+def _uid_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
+    from bls381_amd import comm
+    stub = bytes((7 * k + 3) % 256 for k in range(comm.UID_BYTES))
+    got = comm.exchange_unique_id(rank, world, "127.0.0.1", port, timeout=60.0, make_id=lambda: stub)
+    q.put((rank, got))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_exchange_unique_id_tcp(world):
+    """comm.exchange_unique_id over real sockets at 127.0.0.1: rank 0 serves a stub 128-byte id
+    (RCCL's would need a GPU) and every rank ends with the same bytes.  The non-zero ranks may
+    start before rank 0 listens; they retry until it does."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uid_worker, args=(r, world, port, q)) for r in reversed(range(world))]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(out) == list(range(world))
+    assert len({v for v in out.values()}) == 1 and len(out[0]) == 128
+
+
+def test_exchange_unique_id_times_out_without_rank0():
+    sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
+    from bls381_amd import comm
+    with pytest.raises(TimeoutError):
+        comm.exchange_unique_id(1, 2, "127.0.0.1", _free_port(), timeout=0.5, make_id=lambda: b"\0" * 128)
+
+
+def test_exchange_unique_id_rejects_wrong_size():
+    sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
+    from bls381_amd import comm
+    with pytest.raises(ValueError):
+        comm.exchange_unique_id(0, 2, "127.0.0.1", _free_port(), timeout=0.5, make_id=lambda: b"\0" * 5)
