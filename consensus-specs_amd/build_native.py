@@ -17,7 +17,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 HIP_SOURCES = ["bls381_capi.hip"]
 HEADERS = ["bls381_defs.hpp", "bls381_consts.hpp", "bls381_field.hpp", "bls381_curve.hpp", "bls381_hash.hpp",
-           "bls381_pairing.hpp", "bls381_pair.hpp", "bls381_ssz.hpp", "bls381_kernels.hpp"]
+           "bls381_lazy.hpp", "bls381_pairing.hpp", "bls381_pair.hpp", "bls381_quad.hpp", "bls381_ssz.hpp",
+           "bls381_kernels.hpp"]
 
 
 def _newer(target, deps):

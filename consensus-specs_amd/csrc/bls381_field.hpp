@@ -15,9 +15,14 @@ namespace bls381 {
 #if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
 // host op-count build (tools / bench roofline): Fp multiplications executed
 inline thread_local uint64_t g_fp_mul_count = 0;
+// lazy reduction (bls381_lazy.hpp): a 14x14 product into a wide value and a wide
+// reduction each count as half an Fp multiplication
+inline thread_local uint64_t g_fp_half_count = 0;
 #define BLS_COUNT_FP_MUL() (++g_fp_mul_count)
+#define BLS_COUNT_FP_HALF() (++g_fp_half_count)
 #else
 #define BLS_COUNT_FP_MUL() ((void)0)
+#define BLS_COUNT_FP_HALF() ((void)0)
 #endif
 #if !defined(__HIP_DEVICE_COMPILE__) && !defined(__HIP__)
 // host build: inversions that took fp_inv's fallback (tests assert none do)

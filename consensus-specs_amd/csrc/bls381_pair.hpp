@@ -186,6 +186,25 @@ __device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) { return pr_make(fp_u
 __device__ __forceinline__ bool fp2_is_zero(const fp2p_t& a) { return pr_both(fp_is_zero(a.v)); }
 __device__ __forceinline__ bool fp2_eq(const fp2p_t& a, const fp2p_t& b) { return pr_both(fp_eq(a.v, b.v)); }
 
+// Karabina compressed squaring with lazy reduction (bls381_lazy.hpp): lane p computes
+// coefficient p of every output from both coefficients of the inputs (DPP).  The (g4, g5)
+// outputs come first so only one input pair is read across the lanes at a time.
+__device__ __forceinline__ cyc_bc<fp2p_t> cyc_csqr_lazy(const cyc_bc<fp2p_t>& g) {
+  const bool p = pr_odd();
+  cyc_bc<fp2p_t> r;
+  {
+    const fp_t e4 = pr_dpp<DPP_EVEN>(g.g4.v), o4 = pr_dpp<DPP_ODD>(g.g4.v);
+    const fp_t e5 = pr_dpp<DPP_EVEN>(g.g5.v), o5 = pr_dpp<DPP_ODD>(g.g5.v);
+    r.g2 = pr_make(fp_6p2(lz_xi_mul(p, e4, o4, e5, o5), g.g2.v));
+    r.g3 = pr_make(fp_3m2(lz_sqr_xisqr(p, e4, o4, e5, o5), g.g3.v));
+  }
+  const fp_t e2 = pr_dpp<DPP_EVEN>(g.g2.v), o2 = pr_dpp<DPP_ODD>(g.g2.v);
+  const fp_t e3 = pr_dpp<DPP_EVEN>(g.g3.v), o3 = pr_dpp<DPP_ODD>(g.g3.v);
+  r.g4 = pr_make(fp_3m2(lz_sqr_xisqr(p, e2, o2, e3, o3), g.g4.v));
+  r.g5 = pr_make(fp_6p2(lz_mul(p, e2, o2, e3, o3), g.g5.v));
+  return r;
+}
+
 // 1/a = conj(a) / (a0^2 + a1^2); the norm and its inverse are computed on both lanes
 __device__ inline fp2p_t fp2_inv(const fp2p_t& a) {
   const fp_t t = fp_sqr(a.v);

@@ -341,6 +341,39 @@ __device__ __forceinline__ cq_t cq_compress(const fq12_t& f) {
 
 __device__ __forceinline__ cq_t cq_sqr(const cq_t& g) {
   const bool hi = qd_hi();
+#if BLS_LAZY_CSQR
+  // lazy reduction (bls381_lazy.hpp): each half forms its two outputs from its own (x, y)
+  // as wide sums -- S = x^2 + xi y^2 and lo: xi x y, hi: x y -- one reduction each
+  const bool p = pr_odd();
+  const fp_t ex = pr_dpp<DPP_EVEN>(g.x.v), ox = pr_dpp<DPP_ODD>(g.x.v);
+  const fp_t ey = pr_dpp<DPP_EVEN>(g.y.v), oy = pr_dpp<DPP_ODD>(g.y.v);
+  const fp_t S = lz_sqr_xisqr(p, ex, ox, ey, oy);
+  fp_t P;
+  {
+    lv_t x1, y1, x2, y2;
+#pragma unroll
+    for (int k = 0; k < 14; ++k) {
+      const int32_t b0 = (int32_t)ey.w[k], b1 = (int32_t)oy.w[k];
+      const int32_t s = b0 + b1, d = b0 - b1;
+      x1[k] = (int32_t)ex.w[k];
+      x2[k] = (int32_t)ox.w[k];
+      y1[k] = hi ? (p ? b1 : b0) : (p ? s : d);     // hi: Re/Im(x y), lo: Re/Im(xi x y)
+      y2[k] = hi ? (p ? b0 : -b1) : (p ? d : -s);
+    }
+    wide_t T;
+    wz_init(T);
+    wmac(T, x1, y1);
+    wmac(T, x2, y2);
+    P = wredc(T);
+  }
+  // lo <- hi's (S, x y): g4' = 3 S - 2 g4, g5' = 6 x y + 2 g5;
+  // hi <- lo's (xi x y, S): g2' = 6 xi x y + 2 g2, g3' = 3 S - 2 g3
+  const fp_t So = pr_dpp<DPP_HSWAP>(S), Po = pr_dpp<DPP_HSWAP>(P);
+  cq_t r;
+  r.x = pr_make(fp_6p2_3m2(hi, Po, So, g.x.v));
+  r.y = pr_make(fp_6p2_3m2(!hi, Po, So, g.y.v));
+  return r;
+#else
   const fp2p_t s0 = fp2_sqr(g.x), s1 = fp2_sqr(g.y), s2 = fp2_sqr(fp2_add(g.x, g.y));
   const fp2p_t D = fp2_sub2(s2, s0, s1);       // 2 x y
   const fp2p_t S = fp2_add_mul_xi(s0, s1);     // x^2 + xi y^2
@@ -350,6 +383,7 @@ __device__ __forceinline__ cq_t cq_sqr(const cq_t& g) {
   r.x = fp2_3pm2(U, g.x, !hi);   // lo: g4' = 3 (g2^2 + xi g3^2) - 2 g4;  hi: g2' = 6 xi g4 g5 + 2 g2
   r.y = fp2_3pm2(V, g.y, hi);    // lo: g5' = 6 g2 g3 + 2 g5;             hi: g3' = 3 (g4^2 + xi g5^2) - 2 g3
   return r;
+#endif
 }
 
 // g2 of a compressed value, on all four lanes

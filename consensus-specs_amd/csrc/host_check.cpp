@@ -100,6 +100,15 @@ void hc_fp2_mul_lazy_raw(const uint8_t* x, const uint8_t* y, const uint8_t* z, c
   straw2(o, fp2_mul(fp2_add_lazy(ldraw2(x), ldraw2(y)), fp2_add_lazy(ldraw2(z), ldraw2(u))));
 }
 
+// Karabina compressed squaring (lazy reduction, bls381_lazy.hpp) on raw Montgomery-domain
+// limbs: in/out = (g2, g3, g4, g5) as 4 x 96 bytes, inputs any values < 2q
+void hc_cyc_csqr_raw(const uint8_t* in, uint8_t* out) {
+  cyc_bc<fp2_t> g;
+  g.g2 = ldraw2(in); g.g3 = ldraw2(in + 96); g.g4 = ldraw2(in + 192); g.g5 = ldraw2(in + 288);
+  const cyc_bc<fp2_t> r = cyc_csqr(g);
+  straw2(out, r.g2); straw2(out + 96, r.g3); straw2(out + 192, r.g4); straw2(out + 288, r.g5);
+}
+
 void hc_fp12_mul(const uint8_t* a, const uint8_t* b, uint8_t* o) { st12(o, fp12_mul(ld12(a), ld12(b))); }
 void hc_fp12_sqr(const uint8_t* a, uint8_t* o) { st12(o, fp12_sqr(ld12(a))); }
 void hc_fp12_inv(const uint8_t* a, uint8_t* o) { st12(o, fp12_inv(ld12(a))); }
@@ -287,30 +296,30 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
                            int strict, uint64_t* out) {
   aff_t<fp_t> P;
   aff_t<fp2_t> S, H;
-  g_fp_mul_count = 0;
+  g_fp_mul_count = g_fp_half_count = 0;
   int sp = g1_decompress(P, pk48);
   if (strict && sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
-  out[0] = g_fp_mul_count;
-  g_fp_mul_count = 0;
+  out[0] = g_fp_mul_count + g_fp_half_count / 2;
+  g_fp_mul_count = g_fp_half_count = 0;
   int ss = g2_decompress(S, sig96);
   if (strict && ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
-  out[1] = g_fp_mul_count;
-  g_fp_mul_count = 0;
+  out[1] = g_fp_mul_count + g_fp_half_count / 2;
+  g_fp_mul_count = g_fp_half_count = 0;
   aff_t<fp2_t> c;
   hash_to_g2_candidate(c, msg32, 32, dom8);
   jac_to_aff(H, g2_mul_bp(c));
-  out[2] = g_fp_mul_count;
+  out[2] = g_fp_mul_count + g_fp_half_count / 2;
   if (sp != PT_OK || ss != PT_OK) { out[3] = out[4] = 0; return -1; }
-  g_fp_mul_count = 0;
+  g_fp_mul_count = g_fp_half_count = 0;
   aff_t<fp2_t> Q[2] = {S, H};
   aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
   g1_line_pre Pp[2] = {g1_prepare(ng), g1_prepare(P)};
   bool degen = false;
   const fp12_t f = miller_loop_n<2>(Q, Pp, degen);
-  out[3] = g_fp_mul_count;
-  g_fp_mul_count = 0;
+  out[3] = g_fp_mul_count + g_fp_half_count / 2;
+  g_fp_mul_count = g_fp_half_count = 0;
   const bool ok = fp12_is_one(final_exp(f));
-  out[4] = g_fp_mul_count;
+  out[4] = g_fp_mul_count + g_fp_half_count / 2;
   return ok ? 1 : 0;
 }
 

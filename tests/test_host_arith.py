@@ -167,6 +167,42 @@ def test_fp2_lazy_operands_at_bounds(L):
         assert (r0 % q, r1 % q) == (e[0] * Rinv % q, e[1] * Rinv % q)
 
 
+def _csqr_expect(g, Rinv):
+    """Karabina outputs (cyc_csqr) on Montgomery-domain raw values, mod q."""
+    mm = lambda a, b: tuple(x * Rinv % q for x in M.mul2(a, b))
+    xi = lambda a: ((a[0] - a[1]) % q, (a[0] + a[1]) % q)
+    add = lambda *xs: tuple(sum(x[i] for x in xs) % q for i in range(2))
+    sc = lambda k, a: (k * a[0] % q, k * a[1] % q)
+    g2, g3, g4, g5 = g
+    return (add(sc(6, xi(mm(g4, g5))), sc(2, g2)),
+            add(sc(3, add(mm(g4, g4), xi(mm(g5, g5)))), sc(-2, g3)),
+            add(sc(3, add(mm(g2, g2), xi(mm(g3, g3)))), sc(-2, g4)),
+            add(sc(6, mm(g2, g3)), sc(2, g5)))
+
+
+def test_cyc_csqr_lazy_at_bounds(L):
+    """Lazily reduced Karabina squaring (one signed wide sum per output coefficient) with
+    inputs at the representation's extremes: values up to 2q - 1, normalized limbs all
+    2^28 - 1 where possible.  Outputs < 2q and congruent to the formulas."""
+    rng = random.Random(23)
+    Rinv = pow(1 << 392, -1, q)
+    out = ctypes.create_string_buffer(384)
+    allones = sum((2**28 - 1) << (28 * k) for k in range(13)) + (((2 * q - 1) >> 364) << 364)
+    allones = min(allones, 2 * q - 1)
+    edge = [2 * q - 1, 2 * q - 2, q, q - 1, 0, 1, allones, (1 << 380) - 1]
+    for i in range(600):
+        if i < 256:
+            vals = [edge[(i >> (k % 8)) % len(edge)] if (i + k) % 3 else edge[(i * 7 + k) % len(edge)] for k in range(8)]
+        else:
+            vals = [rng.choice(edge) if rng.random() < 0.3 else rng.randrange(2 * q) for _ in range(8)]
+        g = tuple((vals[2 * j], vals[2 * j + 1]) for j in range(4))
+        L.hc_cyc_csqr_raw(b"".join(b96(x) for x in g), out)
+        got = [i96(out.raw[96 * j:96 * j + 96]) for j in range(4)]
+        for j, e in enumerate(_csqr_expect(g, Rinv)):
+            assert got[j][0] < 2 * q and got[j][1] < 2 * q, (i, j)
+            assert (got[j][0] % q, got[j][1] % q) == e, (i, j)
+
+
 def test_fp12(L):
     rng = random.Random(8)
     buf = ctypes.create_string_buffer(576)
