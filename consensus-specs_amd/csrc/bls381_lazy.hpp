@@ -43,6 +43,18 @@ BLS_INLINE void wmac(wide_t& T, const lv_t& x, const lv_t& y) {
     for (int j = 0; j < 14; ++j) T.c[i + j] += (int64_t)x[i] * (int64_t)y[j];
 }
 
+// T += k x^2 for a small signed k (105 products: cross terms doubled in the multiplier)
+BLS_INLINE void wsqr_k(wide_t& T, const lv_t& x, int32_t k) {
+  BLS_COUNT_FP_HALF();
+#pragma unroll
+  for (int i = 0; i < 14; ++i) {
+    const int32_t d = k * x[i], c = 2 * k * x[i];
+    T.c[2 * i] += (int64_t)d * (int64_t)x[i];
+#pragma unroll
+    for (int j = i + 1; j < 14; ++j) T.c[i + j] += (int64_t)c * (int64_t)x[j];
+  }
+}
+
 // signed Montgomery reduction T 2^-392 mod q (see the header for the bounds)
 BLS_INLINE fp_t wredc(wide_t& T) {
   BLS_COUNT_FP_HALF();
@@ -94,12 +106,10 @@ BLS_INLINE fp_t fp_6p2_3m2(bool six, const fp_t& P, const fp_t& S, const fp_t& x
 //   g4' = 3 (g2^2 + xi g3^2) - 2 g4  g5' = 6 g2 g3 + 2 g5
 // with the products of each output summed in one wide value (lane p = coefficient p):
 //   Re(xi a b) = a0 (b0 - b1) - a1 (b0 + b1)      Im(xi a b) = a0 (b0 + b1) + a1 (b0 - b1)
-//   Re(a^2 + xi b^2) = (a0 + a1)(a0 - a1) + b0 (b0 - 2 b1) - b1 b1
-//   Im(a^2 + xi b^2) = 2 a0 a1 + b0 (b0 + 2 b1) - b1 b1
 //   Re(a b) = a0 b0 - a1 b1                        Im(a b) = a0 b1 + a1 b0
+//   a^2 + xi b^2: lz_sqr_xisqr below
 // Inputs normalized (limbs < 2^28, values < 2q).  Column sums: xi a b and a b hold 28
-// products < 2^57 (2^61.8); a^2 + xi b^2 holds 14 each of < 2^57, < 2^57.6, < 2^56
-// (2^62.4); the reduction adds < 2^59.8.  Values: |X| < 24 q^2.
+// products < 2^57 (2^61.8); the reduction adds < 2^59.8.  Values: |X| < 16 q^2.
 
 // Re/Im of xi a b
 BLS_INLINE fp_t lz_xi_mul(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
@@ -137,24 +147,28 @@ BLS_INLINE fp_t lz_mul(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0, c
   return wredc(T);
 }
 
-// Re/Im of a^2 + xi b^2
+// Re/Im of a^2 + xi b^2, with the xi b^2 part as squares:
+//   Re(xi b^2) = (b0 - b1)^2 - 2 b1^2,  Im(xi b^2) = (b0 + b1)^2 - 2 b1^2
+// (u = b0 -+ b1 reduced first, so its square's columns stay small): 196 + 105 + 105
+// products per lane instead of 3 x 196.  Columns: a-term 14 x 2^57, u^2 7.5 x 2^57,
+// 2 b1^2 7.5 x 2^58, reduction 14 x 2^56: < 2^62.5.  Values in (-16 q^2, 12 q^2).
 BLS_INLINE fp_t lz_sqr_xisqr(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
-  lv_t x1, y1, x2, y2, x3, y3;
+  lv_t x1, y1, u, v;
+  uint32_t s[14];
 #pragma unroll
   for (int k = 0; k < 14; ++k) {
     const int32_t e = (int32_t)a0.w[k], o = (int32_t)a1.w[k];
     x1[k] = e + (p ? e : o);
     y1[k] = p ? o : e - o;
-    x2[k] = (int32_t)b0.w[k];
-    y2[k] = (int32_t)b0.w[k] + (p ? 2 : -2) * (int32_t)b1.w[k];
-    x3[k] = (int32_t)b1.w[k];
-    y3[k] = -(int32_t)b1.w[k];
+    s[k] = b0.w[k] + (p ? b1.w[k] : Q2B_LIMBS[k] - b1.w[k]);
+    v[k] = (int32_t)b1.w[k];
   }
+  lv_from(u, fp_reduce_lc<2>(s));
   wide_t T;
   wz_init(T);
   wmac(T, x1, y1);
-  wmac(T, x2, y2);
-  wmac(T, x3, y3);
+  wsqr_k(T, u, 1);
+  wsqr_k(T, v, -2);
   return wredc(T);
 }
 
