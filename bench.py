@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4/C5 lines")
+    ap.add_argument("--sections", type=str, default="",
+                    help="comma list: run only these secondary lines (deposits, randomized, c3, c4, c5, rccl, latency)")
+    ap.add_argument("--rb-batch", type=str, default="64", help="randomized sub-batch sizes (comma list)")
     ap.add_argument("--c4-keys", type=int, default=1 << 17, help="pubkeys per GPU in the C4 aggregation")
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
@@ -643,7 +646,19 @@ def bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, di
     (nearly every sub-batch then fails: the fallback cost)."""
     import torch
     n = len(pks) // 48
-    B = 64
+    sizes = [int(x) for x in args.rb_batch.split(",") if x]
+    res = {}
+    for B in sizes:
+        res[str(B)] = _bench_randomized_b(native, L, args, pks, msgs, sigs, doms, expected, world, dist, dev,
+                                          stream, t_u8, n, B)
+    out = dict(res[str(sizes[0])])
+    if len(sizes) > 1:
+        out["by_sub_batch"] = res
+    return out
+
+
+def _bench_randomized_b(native, L, args, pks, msgs, sigs, doms, expected, world, dist, dev, stream, t_u8, n, B):
+    import torch
     clean_msgs, clean_sigs = make_workload.clean
     out = {"sub_batch": B}
     ws = torch.empty(L.bls381_verify_batch_randomized_workspace_size(n, B), dtype=torch.uint8, device=dev)
@@ -826,16 +841,23 @@ def main():
         agg["registry"] = bench_registry_c3(native, L, args, pks, idx, offsets, d_out, world, dist, dev, stream, t_u8)
 
     sec = {}
-    if not args.no_secondary:
+    only = set(x for x in args.sections.split(",") if x)
+    want = lambda k: (not args.no_secondary and not only) or k in only
+    if want("deposits"):
         sec["c2_deposits"] = bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8)
+    if want("randomized"):
         sec["c2_randomized_batch"] = bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, dist,
                                                       dev, stream, t_u8)
+    if want("c3"):
         sec["c3_epoch"] = bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist)
+    if want("c4"):
         sec["c4_aggregate"] = bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist)
+    if want("c5"):
         sec["c5_multi_pairing"] = bench_c5(native, args, world, rank, dist, dev)
+    if want("rccl"):
         sec["native_rccl"] = bench_native_comm(native, args, world, rank, dist, dev)
-        if rank == 0:
-            sec["latency"] = bench_latency(native, pks, msgs, sigs, expected)
+    if want("latency") and rank == 0:
+        sec["latency"] = bench_latency(native, pks, msgs, sigs, expected)
 
     if rank != 0:
         if world > 1:

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -289,6 +290,18 @@ bool verify_split(size_t n) { return BLS_ML_SPLIT && n > BLS_ML_QUAD_MAX_N; }
 #ifndef BLS_DECODE_G2_SIDE
 #define BLS_DECODE_G2_SIDE 1
 #endif
+// A/B knobs read once from the environment (measurement only; defaults are the shipped
+// layout): BLS381_G2_ONE_LANE bit 0 = decode_g2, bit 1 = hash_to_g2 on one lane per item.
+// Default 1 (r03k, same box, two runs each): the one-lane decode_g2 beside hash_to_G2 runs
+// 4.1 -> 3.45 ms, C2 2.116 -> 2.133-2.139 M/s; the one-lane hash spills (10 ms against 6.6).
+int env_knob(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : def;
+}
+int g2_one_lane() {
+  static const int v = env_knob("BLS381_G2_ONE_LANE", 1);
+  return v;
+}
 
 int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
                      const uint8_t* doms, uint8_t* verdicts, void* ws, hipStream_t s) {
@@ -302,12 +315,19 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // decode_g1 (one lane per item: one wave per SIMD) and, by default, decode_g2
   // on the side stream, beside hash_to_g2; the Miller loop waits for both branches.
   // Decode waves fill the SIMD slots that finished hash waves free (measured in DESIGN.md §10).
+  // BLS381_C2_ORDER (measurement knob): 1 = the decodes on the side stream beside hash_to_G2,
+  // 0 = everything in sequence on the main stream
+  static const int c2_order = env_knob("BLS381_C2_ORDER", 1);
+  hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  LAUNCH("decode_g1", c->side, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+  LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
 #if BLS_DECODE_G2_SIDE
   // both decodes in sequence beside hash_to_G2
-  LAUNCH("decode_g2", c->side, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
+  if (g2_one_lane() & 1)
+    LAUNCH("decode_g2", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
+  else
+    LAUNCH("decode_g2", sd, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
   HIPC(hipEventRecord(c->ev_join, c->side));
@@ -318,8 +338,11 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   const bool wide = n <= BLS_HASH_WIDE_MAX_N;
   if (wide)
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
-  LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
-         (const uint32_t*)(wide ? w.koff : nullptr), 0);
+  if (!wide && (g2_one_lane() & 2))
+    LAUNCH("hash_to_g2", s, g, b, k_hash_g2_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  else
+    LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
+           (const uint32_t*)(wide ? w.koff : nullptr), 0);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
   if (n <= BLS_ML_OCT_MAX_N) {
     // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
@@ -346,7 +369,7 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
              (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
              w.ml_L, w.ml_st, sig_in_loop ? 1 : 0);
       LAUNCH("miller_accum", s, dim3(grid_for(2 * cnt)), b, k_ml_accum, n, i0, cnt, (const uint32_t*)w.ml_L,
-             (const uint8_t*)w.ml_st, w.f, w.f_st);
+             (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);
     }
   } else {
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
@@ -2496,13 +2519,20 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
 // re-verified item by item with the default pipeline.
 namespace {
 
+// Randomized sub-batches of B items: the items pair up on the split Miller loop's quads
+// (k_rb_ml_lines -> k_ml_accum), so a sub-batch has B/2 item-pair values plus its
+// signature-sum value; the split loop runs in chunks of at most RB_ML_CHUNK item pairs.
+constexpr size_t RB_ML_CHUNK = 32768;
+size_t rb_slots(size_t n, size_t B) { return ((n + B - 1) / B) * (B / 2 + 1); }
+size_t rb_ml_chunk(size_t n, size_t B) { return std::min<size_t>(((n + B - 1) / B) * (B / 2), RB_ML_CHUNK); }
 size_t rb_ws_size(size_t n, size_t B) {
-  const size_t nb = (n + B - 1) / B, nslots = nb * (B + 1);
+  const size_t nb = (n + B - 1) / B, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
   size_t s = verify_ws_size(n) + 4 * 65536;
   s += align256(2 * FPW * n) + 3 * align256(n) + align256(6 * FPW * n) + align256(n);   // R1, statuses, R2, zeros
   const size_t ch = nb + n / CHUNK_L1 + 1;                                              // R2 sums per sub-batch
   s += 3 * (align256(ch * sizeof(agg_chunk)) + align256(ch * 6 * FPW) + align256(ch));
   s += align256(4 * FPW * nb) + align256(nb);                                           // signature sums
+  s += align256(4 * ML_L_WORDS_PER_ITEM * ch_ml) + align256(ch_ml);                     // line products
   s += 2 * (align256(12 * FPW * nslots) + align256(nslots) + align256(nslots * sizeof(agg_chunk)));
   s += 2 * align256(nb) + align256(64);
   s += align256(184 * n) + align256(4 * n) + align256(n) + verify_ws_size(n);           // the per-item fallback
@@ -2512,7 +2542,7 @@ size_t rb_ws_size(size_t n, size_t B) {
 int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
                           const uint8_t* doms, const uint8_t* seed32, size_t B, uint8_t* d_verdicts, void* ws,
                           size_t ws_cap, hipStream_t s, uint64_t* stats) {
-  const size_t nb = (n + B - 1) / B, nslots = nb * (B + 1);
+  const size_t nb = (n + B - 1) / B, hb = B / 2, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
   Bump b(ws, ws_cap);
   VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n)), n);
   uint32_t* r1 = b.take<uint32_t>(2 * FP_LIMBS * n);
@@ -2526,9 +2556,11 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   auto seed = std::make_shared<std::vector<uint8_t>>(seed32, seed32 + 32);
   HIPC(hipMemcpyAsync(d_seed, seed->data(), 32, hipMemcpyHostToDevice, s));
   HIPC(hipMemsetAsync(zeros, 0, n, s));
-  // Miller values: B item slots per sub-batch + its signature-sum slot
+  // Miller values: B/2 item-pair slots per sub-batch + its signature-sum slot
   uint32_t* f = b.take<uint32_t>(12 * FP_LIMBS * nslots);
   uint8_t* fst = b.take<uint8_t>(nslots);
+  uint32_t* mlL = b.take<uint32_t>(ML_L_WORDS_PER_ITEM * ch_ml);
+  uint8_t* mlst = b.take<uint8_t>(ch_ml);
   // per sub-batch sum of [r_i] sig_i (planned here; runs on the side stream)
   std::vector<uint32_t> off(nb + 1);
   for (size_t k = 0; k <= nb; ++k) off[k] = (uint32_t)std::min(n, k * B);
@@ -2536,45 +2568,64 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   uint32_t* s_aff = b.take<uint32_t>(4 * FP_LIMBS * nb);
   uint8_t* s_st = b.take<uint8_t>(nb);
   {
-    // Order: the signature branch first ([r_i] sig_i and the sub-batch sums, throughput
-    // launches on the main stream), then its 1,024-odd latency-bound sum Miller loops on
-    // the high-priority stream beside hash_to_G2 (their waves are dispatched first, the
-    // hash fills the rest of the chip), then [r_i] pk_i and the per-item loops, which join
-    // the sums' loops before the segmented products.  Everything else runs in sequence:
-    // the launches are whole rounds of waves (2n lanes, or n for the one-lane kernels), and
-    // overlapping two of them (decode_g1 beside decode_g2, [r_i] pk_i beside [r_i] sig_i)
-    // measured slower -- a second, partial round.
+    // Order, BLS381_RB_ORDER (measurement knob):
+    //  0 (default): everything in sequence on the main stream, except the sub-batch sums'
+    //    latency-bound Miller loops (high-priority stream, beside hash_to_G2).
+    //  1: hash_to_G2 on the main stream, the signature branch (decode_g1, decode_g2,
+    //    [r_i] sig_i, the sums) and [r_i] pk_i beside it on the side stream: measured r03j,
+    //    30.3 against 28.1 ms per clean 2^16 batch (two different large kernels co-resident).
     std::lock_guard<std::mutex> lk(c->fork_mu);
-    LAUNCH("decode_g1", s, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    static const int order = env_knob("BLS381_RB_ORDER", 0);
+    hipStream_t sb = s;
+    if (order == 1) {
+      sb = c->side;
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(sb, c->ev_fork, 0));
+      LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
+             (const uint32_t*)nullptr, 0);
+    }
+    LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
     // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-    LAUNCH("decode_g2", s, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
-    LAUNCH("rb_scale_g2", s, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
+    LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
+    LAUNCH("rb_scale_g2", sb, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
            (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
     const uint32_t* sjac;
     const uint8_t* sbad;
     size_t used = 0;
     uint8_t* sub = b.take<uint8_t>(0);
-    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, s, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
+    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, sb, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
       return e;
     b.off += used;
-    LAUNCH("agg_g2_affine", s, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
-    HIPC(hipEventRecord(c->ev_fork, s));
-    HIPC(hipStreamWaitEvent(c->prio, c->ev_fork, 0));
-    LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, B, (const uint32_t*)s_aff,
+    LAUNCH("agg_g2_affine", sb, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
+    HIPC(hipEventRecord(c->ev_join, sb));
+    HIPC(hipStreamWaitEvent(c->prio, c->ev_join, 0));
+    LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
-    LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
-           (const uint32_t*)nullptr, 0);
-    LAUNCH("rb_scale_g1", s, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
+    if (order != 1)
+      LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
+             (const uint32_t*)nullptr, 0);
+    LAUNCH("rb_scale_g1", sb, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
            (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
+    if (order == 1) {
+      HIPC(hipEventRecord(c->ev_join, sb));
+      HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    }
+    // the batched items two per Miller accumulator: lines of both pairs on a quad, then f^2 L
+    // on quads (2^15 accumulators per 2^16 items: a pair launch would leave SIMDs half empty)
+    const size_t nq = nb * hb;
+    for (size_t q0 = 0; q0 < nq; q0 += ch_ml) {
+      const size_t cnt = std::min(ch_ml, nq - q0);
+      LAUNCH("rb_miller_lines", s, dim3(grid_for(4 * cnt)), blk, k_rb_ml_lines, n, q0, cnt, (const uint32_t*)w.h_aff,
+             (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st, (const uint8_t*)cls, mlL, mlst);
+      LAUNCH("rb_miller_accum", s, dim3(grid_for(4 * cnt)), blk, k_ml_accum_q, nslots, q0, cnt, (const uint32_t*)mlL,
+             (const uint8_t*)mlst, f, fst, hb);
+    }
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
-    LAUNCH("rb_miller_items", s, dim3(grid_for(2 * nb * B)), blk, k_rb_miller_items, n, B, nb * B,
-           (const uint32_t*)w.h_aff, (const uint8_t*)w.f_st, (const uint32_t*)r1, (const uint8_t*)r1_st,
-           (const uint8_t*)cls, nslots, f, fst);
   }
   int rc = 0;
   std::vector<uint32_t> seg(nb + 1);
-  for (size_t k = 0; k <= nb; ++k) seg[k] = (uint32_t)(k * (B + 1));
+  for (size_t k = 0; k <= nb; ++k) seg[k] = (uint32_t)(k * (hb + 1));
   auto passes = std::make_shared<std::vector<std::vector<agg_chunk>>>(plan_products(seg));
   size_t n_in = nslots;
   for (const auto& chunks : *passes) {

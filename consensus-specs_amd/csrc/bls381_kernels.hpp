@@ -167,6 +167,40 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2(size_t n, 
   if (fin) soa_st_g2(out, n, i, h);
 }
 
+// One-lane forms of decode_g2 and hash_to_g2 (fp2_t arithmetic on one lane per item:
+// Karatsuba Fp2 products, and the Fp-only square roots computed once per item instead of
+// on both lanes of a pair).  They write the lane-pair SoA layout the pair kernels read.
+__device__ __forceinline__ void soa_st_g2_1(uint32_t* p, size_t n, size_t i, const aff_t<fp2_t>& a) {
+  soa_st(p, 2 * n, 2 * i, 0, a.x.c0); soa_st(p, 2 * n, 2 * i + 1, 0, a.x.c1);
+  soa_st(p, 2 * n, 2 * i, 1, a.y.c0); soa_st(p, 2 * n, 2 * i + 1, 1, a.y.c1);
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t n, const uint8_t* __restrict__ sigs,
+                                                       uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                       int check_subgroup) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  aff_t<fp2_t> a;
+  int s = g2_decompress(a, sigs + 96 * i);
+  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = check_subgroup == 2 ? ST_NOSUB : PT_BAD;
+  st[i] = (uint8_t)s;
+  if (s == PT_OK || s == ST_NOSUB) soa_st_g2_1(out, n, i, a);
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_1(size_t n, const uint8_t* __restrict__ msgs,
+                                                     uint32_t mlen, const uint8_t* __restrict__ doms,
+                                                     int dom_stride, uint32_t* __restrict__ out,
+                                                     uint8_t* __restrict__ st) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  uint8_t dom[8];
+  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
+  aff_t<fp2_t> h;
+  const bool fin = jac_to_aff(h, g2_mul_bp(c));
+  if (st) st[i] = fin ? ST_OK : ST_INF;
+  if (fin) soa_st_g2_1(out, n, i, h);
+}
+
 // The latency form of the try-and-increment search (bls_signature.md:74-86): W lanes per
 // message test candidates x + k, x + k + 1, ..., one Legendre symbol each (one-lane Fp2
 // arithmetic), and the item's lowest square offset is taken from a ballot; with W = 16 a
@@ -376,14 +410,17 @@ __device__ __forceinline__ fp12p_t ml_load_L(const uint32_t* __restrict__ L, siz
 }
 
 // f = conj(prod_j L_j^(2^(later doublings))) for items i0 .. i0 + cnt - 1; writes f (SoA over n
-// items, the layout k_final_exp_verdict reads) and the item status
+// items, the layout k_final_exp_verdict reads) and the item status.  grp > 0 (randomized
+// batches): item i's value goes to slot (i / grp) (grp + 1) + i % grp of n slots, so every
+// group of grp values leaves a slot free after it (the signature-sum value of a sub-batch).
 __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t n, size_t i0, size_t cnt,
                                                     const uint32_t* __restrict__ L,
                                                     const uint8_t* __restrict__ st_in,
-                                                    uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+                                                    uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out,
+                                                    size_t grp) {
   const size_t li = item_index<2>();
   if (li >= cnt) return;
-  const size_t i = i0 + li;
+  const size_t i = grp ? ((i0 + li) / grp) * (grp + 1) + (i0 + li) % grp : i0 + li;
   const bool lead = !pr_odd();
   const uint8_t s = st_in[li];
   if (s == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
@@ -401,6 +438,52 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t
     f = fp12_conj(f);
   }
   soa_st12(f_out, n, i, f);
+  if (lead) st_out[i] = ST_OK;
+}
+
+// k_ml_accum on lane quads (bls381_quad.hpp: lo holds f's Fp6 half c0, hi c1), for launches
+// with too few accumulators to fill the chip on lane pairs (randomized sub-batches: two
+// items per accumulator, so 2^16 items give 2^15 of them -- 1,024 pair waves, one per
+// SIMD, against 2,048 quad waves).  Same L input, same output layout (pair SoA), same grp.
+__device__ __noinline__ fq12_t ml_accum_q_run(const uint32_t* __restrict__ L, size_t cnt, size_t li) {
+  const bool hi = qd_hi();
+  const size_t col = 2 * li + (pr_odd() ? 1 : 0);
+  auto load = [&](int j) {
+    const int c = j * ML_LC;
+    fq12_t r;
+    r.h.c0 = hi ? e2_zero<fp2p_t>() : pr_make(soa_ld(L, 2 * cnt, col, c + 0));
+    r.h.c1 = pr_make(soa_ld(L, 2 * cnt, col, c + (hi ? 3 : 1)));
+    r.h.c2 = pr_make(soa_ld(L, 2 * cnt, col, c + (hi ? 4 : 2)));
+    return r;
+  };
+  fq12_t f = load(0);
+  int j = 1;
+  if ((BLS_X_ABS >> 62) & 1) f = fq12_mul(f, load(j++));
+  for (int b = 61; b >= 0; --b) {
+    f = fq12_mul(fq12_sqr(f), load(j++));
+    if ((BLS_X_ABS >> b) & 1) f = fq12_mul(f, load(j++));
+  }
+  return fq12_conj(f);
+}
+
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum_q(size_t n, size_t i0, size_t cnt,
+                                                      const uint32_t* __restrict__ L,
+                                                      const uint8_t* __restrict__ st_in,
+                                                      uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out,
+                                                      size_t grp) {
+  const size_t li = item_index<4>();
+  if (li >= cnt) return;
+  const size_t i = grp ? ((i0 + li) / grp) * (grp + 1) + (i0 + li) % grp : i0 + li;
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const uint8_t s = st_in[li];
+  if (s == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
+  // the quad's lanes: lo pair reads L's lane-pair slot li (both halves read slot li)
+  const fq12_t f = (s == ML_ST_ONE) ? fq12_one() : ml_accum_q_run(L, cnt, li);
+  const int p = pr_odd() ? 1 : 0;
+  const int c0 = qd_hi() ? 3 : 0;
+  soa_st(f_out, 2 * n, 2 * i + p, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 2 * n, 2 * i + p, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 2 * n, 2 * i + p, c0 + 2, f.h.c2.v);
   if (lead) st_out[i] = ST_OK;
 }
 
@@ -630,41 +713,54 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g2_affine(size
   if (lead) st[g] = ST_OK;
 }
 
-// Miller values of one sub-batch layout: sub-batch b owns slots [b (B + 1), (b + 1)(B + 1)):
-// B item slots (item bB + k at slot b (B + 1) + k, its pair (H, R1), one item per lane
-// pair: 2n lanes, two waves per SIMD at 2^16 items) and the signature-sum slot.  Item
-// slots past the last item, and items outside the batch, hold 1.
-__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_items(size_t n, size_t B, size_t nitem_slots,
-                                                           const uint32_t* __restrict__ h_aff,
-                                                           const uint8_t* __restrict__ h_st,
-                                                           const uint32_t* __restrict__ r1_aff,
-                                                           const uint8_t* __restrict__ r1_st,
-                                                           const uint8_t* __restrict__ cls, size_t nslots,
-                                                           uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t i = item_index<2>();
-  if (i >= nitem_slots) return;
-  const size_t slot = (i / B) * (B + 1) + i % B;
-  fp12p_t f = fp12_one<fp2p_t>();
-  bool degen = false;
-  if (i < n && cls[i] == RB_BATCH && r1_st[i] == ST_OK && h_st[i] == ST_OK) {
-    const aff_t<fp2p_t> Q = soa_ld_g2(h_aff, n, i);
-    const g1_line_pre P = g1_prepare(soa_ld_g1(r1_aff, n, i));
-    f = miller_loop_n<1>(&Q, &P, degen);
-  }
-  soa_st12(f_out, nslots, slot, f);
-  if (!pr_odd()) st_out[slot] = degen ? ST_BAD : ST_OK;
+// Randomized batches, split Miller loop (the C2 kernels' layout): quad q runs the pairs
+// (BP(H_i), [r_i] pk_i) of items i = 2q (lo half) and 2q + 1 (hi half) and writes their line
+// products L = l l' for k_ml_accum, so two batched items share one f and its squarings.  A
+// half whose item is not batched (not RB_BATCH, an infinite [r_i] pk_i or hash) idles with its
+// lines masked to 1.  Status per quad: ML_ST_ONE (both idle), ST_BAD (a degenerate loop: the
+// sub-batch then fails and its items go one by one), else ST_OK.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(size_t n, size_t q0, size_t cnt,
+                                                       const uint32_t* __restrict__ h_aff,
+                                                       const uint8_t* __restrict__ h_st,
+                                                       const uint32_t* __restrict__ r1_aff,
+                                                       const uint8_t* __restrict__ r1_st,
+                                                       const uint8_t* __restrict__ cls,
+                                                       uint32_t* __restrict__ L, uint8_t* __restrict__ st_out) {
+  const size_t lq = item_index<4>();
+  if (lq >= cnt) return;
+  const size_t q = q0 + lq;
+  const bool hi = qd_hi();
+  const bool lead = (threadIdx.x & 3u) == 0;
+  const size_t ia = 2 * q, ib = 2 * q + 1;
+  const bool a_ok = ia < n && cls[ia] == RB_BATCH && r1_st[ia] == ST_OK && h_st[ia] == ST_OK;
+  const bool b_ok = ib < n && cls[ib] == RB_BATCH && r1_st[ib] == ST_OK && h_st[ib] == ST_OK;
+  if (!a_ok && !b_ok) { if (lead) st_out[lq] = ML_ST_ONE; return; }
+  // an idle half runs the other half's pair with its lines masked to 1
+  const bool active = hi ? b_ok : a_ok;
+  const size_t i = (hi ? b_ok : !a_ok) ? ib : ia;
+  const size_t lp = 2 * i + (pr_odd() ? 1 : 0);
+  aff_t<fp2p_t> Q;
+  Q.x = pr_make(soa_ld(h_aff, 2 * n, lp, 0));
+  Q.y = pr_make(soa_ld(h_aff, 2 * n, lp, 1));
+  const g1_line_pre pre = g1_prepare(soa_ld_g1(r1_aff, n, i));
+  g2_proj<fp2p_t> T;
+  ml_lines_run(Q, pre, active, L, cnt, lq, T);
+  bool bad = active && fp2_is_zero(T.z);
+  bad = !qd_all(!bad);
+  if (lead) st_out[lq] = bad ? ST_BAD : ST_OK;
 }
 
 // the signature-sum slot of every sub-batch: (sum_i [r_i] sig_i, -[c] g1), one lane quad
 // per sub-batch (miller_loop_q1, the latency form: nb is small and this branch runs
 // beside the per-item work)
-__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t B,
+// (slot_per: the item value slots per sub-batch; the sum's slot follows them)
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t slot_per,
                                                          const uint32_t* __restrict__ s_aff,
                                                          const uint8_t* __restrict__ s_st, size_t nslots,
                                                          uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
   const size_t b = item_index<4>();
   if (b >= nb) return;
-  const size_t slot = b * (B + 1) + B;
+  const size_t slot = b * (slot_per + 1) + slot_per;
   const int p = pr_odd() ? 1 : 0;
   fq12_t f = fq12_one();
   bool degen = false;

@@ -97,6 +97,39 @@ __global__ void __launch_bounds__(128, 2) k_fp2_mul(size_t nl, int reps, const u
   KTAIL
 }
 
+// whole exponentiation by x / whole final exponentiation, one per item
+__device__ __forceinline__ fp12_g<fp2p_t> ld12(const uint32_t* p, size_t nl, size_t lane) {
+  fp12_g<fp2p_t> f;
+  f.c0.c0.v = ld(p, nl, lane, 0); f.c0.c1.v = ld(p, nl, lane, 1); f.c0.c2.v = ld(p, nl, lane, 2);
+  f.c1.c0.v = ld(p, nl, lane, 3); f.c1.c1.v = ld(p, nl, lane, 4); f.c1.c2.v = ld(p, nl, lane, 5);
+  return f;
+}
+__device__ __forceinline__ void st12(uint32_t* p, size_t nl, size_t lane, const fp12_g<fp2p_t>& f) {
+  st(p, nl, lane, 0, f.c0.c0.v); st(p, nl, lane, 1, f.c0.c1.v); st(p, nl, lane, 2, f.c0.c2.v);
+  st(p, nl, lane, 3, f.c1.c0.v); st(p, nl, lane, 4, f.c1.c1.v); st(p, nl, lane, 5, f.c1.c2.v);
+}
+__global__ void __launch_bounds__(128, 2) k_cyc_exp_x(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nl) return;
+  fp12_g<fp2p_t> f = ld12(in, nl, lane);
+  for (int i = 0; i < reps; ++i) f = cyc_exp_x(f);
+  st12(out, nl, lane, f);
+}
+__global__ void __launch_bounds__(128, 2) k_final_exp(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nl) return;
+  fp12_g<fp2p_t> f = ld12(in, nl, lane);
+  for (int i = 0; i < reps; ++i) f = final_exp(f);
+  st12(out, nl, lane, f);
+}
+__global__ void __launch_bounds__(128, 2) k_fp12_mul(size_t nl, int reps, const uint32_t* in, uint32_t* out) {
+  const size_t lane = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= nl) return;
+  fp12_g<fp2p_t> f = ld12(in, nl, lane), g = ld12(in + 6 * 14 * nl / 2, nl / 2, lane / 2);
+  for (int i = 0; i < reps; ++i) f = fp12_mul_inl(f, g);
+  st12(out, nl, lane, f);
+}
+
 constexpr int ITERS = 4096;
 __global__ __launch_bounds__(256) void k_mad_u64(uint64_t* o, uint32_t seed) {
   uint32_t a = seed + threadIdx.x, b = seed * 3u + blockIdx.x;
@@ -133,7 +166,7 @@ __global__ __launch_bounds__(256) void k_mad_i64(uint64_t* o, uint32_t seed) {
 
 int main() {
   const size_t n = 1 << 16, nl = 2 * n;
-  std::vector<uint32_t> h(4 * 14 * nl);
+  std::vector<uint32_t> h(12 * 14 * nl);
   uint64_t x = 88172645463325252ull;
   for (auto& v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = (uint32_t)x; }
   uint32_t *in, *out;
@@ -160,6 +193,9 @@ int main() {
   time("csqr_lazy_fenced", k_csqr_lazy_fenced, 63);
   time("lz_mul", k_lz_mul, 63);
   time("fp2_mul", k_fp2_mul, 63);
+  time("cyc_exp_x", k_cyc_exp_x, 1);
+  time("fp12_mul", k_fp12_mul, 16);
+  time("final_exp", k_final_exp, 1);
   uint64_t* o;
   CHECK(hipMalloc(&o, 1024 * 256 * 8 * 8));
   auto rate = [&](const char* name, void (*k)(uint64_t*, uint32_t)) {
