@@ -109,8 +109,11 @@ def load_valu_peak():
 
 
 # profile key (bls381_profile_read) -> kernel symbol in rocprofv3 / PMC output
-PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2", "hash_to_g2": "k_hash_g2",
-                  "miller_loop_2": "k_miller_verify", "final_exp": "k_final_exp_verdict"}
+PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2_1", "hash_to_g2": "k_hash_g2",
+                  "miller_loop_2": "k_miller_verify", "final_exp": "k_final_exp_verdict",
+                  "miller_lines": "k_ml_lines", "miller_accum": "k_ml_accum"}
+# the C2 batch (2^16 items) runs the split Miller loop: the monolithic count is not part of its pipeline
+PIPELINE_STAGES = ["decode_g1", "decode_g2", "hash_to_g2", "miller_lines", "miller_accum", "final_exp"]
 
 
 def load_pmc_traffic(prof_key, n):
@@ -174,18 +177,37 @@ def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
     import build_native
     path = build_native.build_hostcheck(count_ops=True)
     L = ctypes.CDLL(path)
-    tot = np.zeros(5)
+    tot = np.zeros(7)
     done = 0
     for i in range(64):
-        out = (ctypes.c_uint64 * 5)()
+        out = (ctypes.c_uint64 * 7)()
         if L.hc_count_verify_stages(pks[48 * i:48 * i + 48], msgs[32 * i:32 * i + 32],
                                     sigs[96 * i:96 * i + 96], doms[8 * i:8 * i + 8], strict, out) == 1:
             tot += np.array(list(out), dtype=float)
             done += 1
             if done == k:
                 break
-    names = ["decode_g1", "decode_g2", "hash_to_g2", "miller_loop_2", "final_exp"]
+    names = ["decode_g1", "decode_g2", "hash_to_g2", "miller_loop_2", "final_exp", "miller_lines", "miller_accum"]
     return {nm: tot[j] / done for j, nm in enumerate(names)}
+
+
+def agg_roofline(aprof, sample_pks, k, keys):
+    """Roofline of the committee aggregation's dominant kernel: Fp multiplications per key of
+    decode + add (the -DBLS_COUNT_OPS host build, hc_count_aggregate over one committee) x keys x
+    300 MACs, over that kernel's HIP-event time; the same integer-VALU peak as the C2 line."""
+    import build_native
+    L = ctypes.CDLL(build_native.build_hostcheck(count_ops=True))
+    out = ctypes.c_uint64()
+    if L.hc_count_aggregate(ctypes.c_size_t(k), sample_pks, ctypes.byref(out)) != 0:
+        return None
+    per_key = out.value / k
+    ms = {kk: v["total_ms"] / v["count"] for kk, v in aprof.items()}
+    dom = max(ms, key=ms.get)
+    peak, _ = load_valu_peak()
+    ach = per_key * MACS_PER_FP_MUL * keys / (ms[dom] * 1e-3) / 1e12
+    return {"kernel": dom, "fp_mul_per_key": round(per_key, 1), "kernel_avg_ms": ms,
+            "achieved": round(ach, 3), "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
+            "frac": round(ach / peak, 4) if peak else None}
 
 
 def _cpu_verify(args):
@@ -467,15 +489,18 @@ def bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    native.profile_enable(True)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
     t = _max_time(time.perf_counter() - t0, world, dist, dev)
+    cprof = native.profile_read()
+    native.profile_enable(False)
     out = {"workload": "C4: %d pubkeys per GPU (%d total) -> one bls_aggregate_pubkeys; per-GPU partial, "
                        "all-gather, sum on rank 0" % (k, k * world),
            "pubkeys_aggregated_per_s": k * world * steps / t, "ms_per_aggregate": 1e3 * t / steps,
-           "n_gpus": world}
+           "n_gpus": world, "roofline": agg_roofline(cprof, pk[:48 * 128], 128, k)}
     out["registry"] = bench_c4_registry(native, L, args, world, rank, dev, stream, t_u8, dist)
     return out
 
@@ -824,11 +849,14 @@ def main():
         if world > 1:
             dist.barrier()
         a_steps = max(args.steps, 3)
+        native.profile_enable(True)
         t0 = time.perf_counter()
         for _ in range(a_steps):
             astep()
         torch.cuda.synchronize()
         at = time.perf_counter() - t0
+        aprof = native.profile_read()
+        native.profile_enable(False)
         if world > 1:
             t = torch.tensor([at], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -837,7 +865,8 @@ def main():
         agg = {"workload": "C3: %d committees x %d pubkeys, bls_aggregate_pubkeys each" % (nc, cs),
                "committee_aggregations_per_s": nc * a_steps * world / at,
                "pubkeys_aggregated_per_s": nc * cs * a_steps * world / at,
-               "ms_per_step": 1e3 * at / a_steps}
+               "ms_per_step": 1e3 * at / a_steps,
+               "roofline": agg_roofline(aprof, cpks[:48 * cs], cs, nc * cs)}
         agg["registry"] = bench_registry_c3(native, L, args, pks, idx, offsets, d_out, world, dist, dev, stream, t_u8)
 
     sec = {}
@@ -881,7 +910,7 @@ def main():
                 "peak_source": peak_src}
     # the whole pipeline's work over the timed step's wall time (kernels on the side stream overlap
     # the main stream, so the sum of kernel times would double-count them)
-    whole = sum(counts.values()) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
+    whole = sum(counts[k] for k in PIPELINE_STAGES) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
     roofline["pipeline_achieved"] = round(whole, 3)
     roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
     roofline["issue"] = issue_roofline(dom_k, n, kern_ms[dom_k])

@@ -320,6 +320,33 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   g_fp_mul_count = g_fp_half_count = 0;
   const bool ok = fp12_is_one(final_exp(f));
   out[4] = g_fp_mul_count + g_fp_half_count / 2;
+  // the split Miller loop of the throughput path, per kernel (bls381_kernels.hpp):
+  // out[5] k_ml_lines (both running points, L = l l'), out[6] k_ml_accum (f^2 L)
+  uint64_t lines = 0, accum = 0;
+  g2_proj<fp2_t> T[2];
+  for (int k = 0; k < 2; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = fp2_one(); }
+  fp12_t g;
+  int step = 0;
+  auto run_step = [&](bool add) {
+    fp2_t c[3], d[3];
+    g_fp_mul_count = g_fp_half_count = 0;
+    if (add) { line_add(T[0], Q[0], Pp[0], c[0], c[1], c[2]); line_add(T[1], Q[1], Pp[1], d[0], d[1], d[2]); }
+    else { line_dbl(T[0], Pp[0], c[0], c[1], c[2]); line_dbl(T[1], Pp[1], d[0], d[1], d[2]); }
+    const fp12_t L = line_pair_product(c[0], c[1], c[2], d[0], d[1], d[2]);
+    lines += g_fp_mul_count + g_fp_half_count / 2;
+    g_fp_mul_count = g_fp_half_count = 0;
+    if (step == 0) g = L;
+    else if (add || step == 1) g = fp12_mul_by_line_pair_inl(g, L);
+    else g = fp12_mul_by_line_pair_inl(fp12_sqr_inl(g), L);
+    accum += g_fp_mul_count + g_fp_half_count / 2;
+    ++step;
+  };
+  for (int b = 62; b >= 0; --b) {
+    run_step(false);
+    if ((BLS_X_ABS >> b) & 1) run_step(true);
+  }
+  out[5] = lines;
+  out[6] = accum;
   return ok ? 1 : 0;
 }
 

@@ -13,7 +13,7 @@ timeout -k 10 600 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --
  && echo "smoke ok" \
  && timeout -k 10 900 python bench.py --steps $STEPS --warmup 1 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
  && echo "bench ok" && cat gpurun_out/bench_$TAG.json \
- && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o prof -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/rocprof_$TAG.log 2>&1 \
+ && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o prof -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary > gpurun_out/rocprof_$TAG.log 2>&1 \
  && echo "rocprof ok"
 rc=$?
 tail -5 gpurun_out/gpu_tests_$TAG.log

@@ -34,6 +34,21 @@ def main():
                                                   ctypes.c_void_p(s.cuda_stream)))
     torch.cuda.synchronize()
     assert np.array_equal(ver.cpu().numpy().astype(bool), expected)
+    # C3 committee aggregation (1024 x 128 keys drawn from the batch): k_agg_chunks + k_agg_compress
+    nc, cs = 1024, 128
+    idx = np.random.default_rng(3).integers(0, n, nc * cs)
+    cpks = np.frombuffer(pks, dtype=np.uint8).reshape(n, 48)[idx].tobytes()
+    off = np.arange(0, nc * cs + 1, cs, dtype=np.uint32)
+    d_c = t(cpks)
+    d_out = torch.zeros(nc * 48, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(nc, dtype=torch.int32, device=dev)
+    aws = torch.empty(L.bls381_aggregate_pubkeys_batch_workspace_size(nc, nc * cs), dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        native.check(L.bls381_aggregate_pubkeys_batch_device(nc, off.ctypes.data_as(ctypes.c_void_p), nc * cs,
+                                                             d_c.data_ptr(), d_out.data_ptr(), d_st.data_ptr(),
+                                                             aws.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    torch.cuda.synchronize()
+    assert int(d_st.abs().sum().item()) == 0
     print("prof workload ok", n)
 
 
