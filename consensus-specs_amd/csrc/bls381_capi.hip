@@ -57,7 +57,7 @@ struct Ctx {
   // high-priority stream: small latency-bound launches whose waves should be dispatched
   // ahead of a large launch queued at the same time on another stream
   hipStream_t prio = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr, ev_join3 = nullptr;
   std::mutex fork_mu;
   void* ws = nullptr;
   size_t ws_cap = 0;
@@ -120,7 +120,8 @@ Ctx* get_ctx(int* rc) {
         hipStreamCreateWithPriority(&c->prio, hipStreamNonBlocking, prio_hi) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join3, hipEventDisableTiming) != hipSuccess) {
       delete c; t_err = "stream create failed"; *rc = BLS381_EHIP; return nullptr;
     }
     g_ctx[dev] = c;
@@ -302,6 +303,32 @@ int g2_one_lane() {
   static const int v = env_knob("BLS381_G2_ONE_LANE", 1);
   return v;
 }
+// hash_to_G2 of throughput batches as k_hash_cand_1 (search + root, one lane per item) then
+// k_hash_bp (cofactor map, lane pairs); BLS381_HASH_SPLIT=0: the one pair kernel k_hash_g2
+int hash_split() {
+  static const int v = env_knob("BLS381_HASH_SPLIT", 1);
+  return v;
+}
+// hash_to_G2 of n messages (throughput form, no precomputed search offsets) into h_aff, status
+// into st (may be null); prio as k_hash_g2's
+int launch_hash_g2(hipStream_t s, size_t n, const uint8_t* msgs, uint32_t mlen, const uint8_t* doms, int dom_stride,
+                   uint32_t* h_aff, uint8_t* st, int prio = 0) {
+  if (hash_split() && !prio) {
+    LAUNCH("hash_cand", s, dim3(grid_for(n)), dim3(KBLOCK), k_hash_cand_1, n, msgs, mlen, doms, dom_stride, h_aff);
+    LAUNCH("hash_bp", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_hash_bp, n, h_aff, st);
+    return 0;
+  }
+  LAUNCH("hash_to_g2", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_hash_g2, n, msgs, mlen, doms, dom_stride, h_aff, st,
+         (const uint32_t*)nullptr, prio);
+  return 0;
+}
+#define LAUNCH_HASH(...)                        \
+  do {                                          \
+    int rc__ = launch_hash_g2(__VA_ARGS__);     \
+    if (rc__) return rc__;                      \
+  } while (0)
+
+int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStream_t s, bool sig_in_loop);
 
 int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
                      const uint8_t* doms, uint8_t* verdicts, void* ws, hipStream_t s) {
@@ -340,10 +367,20 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
   if (!wide && (g2_one_lane() & 2))
     LAUNCH("hash_to_g2", s, g, b, k_hash_g2_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
+  else if (!wide)
+    LAUNCH_HASH(s, n, msgs, 32u, doms, 8, w.h_aff, (uint8_t*)nullptr);
   else
     LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
-           (const uint32_t*)(wide ? w.koff : nullptr), 0);
+           (const uint32_t*)w.koff, 0);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+  return run_verify_pairings(n, w, verdicts, s, sig_in_loop);
+}
+
+// The verify batch after its decodes and hash: Miller loops and final exponentiation over
+// the decoded points in `w` (statuses pk_st / sig_st, hash points h_aff), verdicts out.
+// sig_in_loop: the strict policy's G2 test of the signatures is still to be done (in the loop).
+int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStream_t s, bool sig_in_loop) {
+  const dim3 g2(grid_for(2 * n)), b(KBLOCK);
   if (n <= BLS_ML_OCT_MAX_N) {
     // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
     LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
@@ -877,6 +914,30 @@ __global__ void __launch_bounds__(KBLOCK) k_gather_rows(size_t n, const uint32_t
   dst[t] = src[(size_t)idx[k] * row_bytes + b];
 }
 
+// items idx[k] of SoA arrays with `rows` rows of n*e words (e words per item: 1 for G1
+// coordinates, 2 for the lane-pair G2 layout) -> item k of the same layout over m items
+__global__ void __launch_bounds__(KBLOCK) k_gather_soa(size_t m, const uint32_t* __restrict__ idx,
+                                                       const uint32_t* __restrict__ src, size_t n, uint32_t rows,
+                                                       uint32_t e, uint32_t* __restrict__ dst) {
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= m * e * rows) return;
+  const size_t r = t / (m * e), ke = t % (m * e), k = ke / e, j = ke % e;
+  dst[t] = src[r * n * e + (size_t)idx[k] * e + j];
+}
+// statuses of the gathered items; a signature outside G2 that decoded (ST_NOSUB, py_ecc
+// policy) is an ordinary point to the per-item loops, as in the default decode
+__global__ void __launch_bounds__(KBLOCK) k_gather_st(size_t m, const uint32_t* __restrict__ idx,
+                                                      const uint8_t* __restrict__ pk_st,
+                                                      const uint8_t* __restrict__ sig_st,
+                                                      uint8_t* __restrict__ pk_out, uint8_t* __restrict__ sig_out) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= m) return;
+  const size_t i = idx[k];
+  pk_out[k] = pk_st[i];
+  const uint8_t ss = sig_st[i];
+  sig_out[k] = ss == ST_NOSUB ? ST_OK : ss;
+}
+
 // Runs a planned batch up to (and excluding) the final exponentiation: keys,
 // signatures and domains are device buffers (d_pks indexed by the caller's key
 // numbering); the plan's own arrays are copied here.  Returns per-call Fp12
@@ -972,9 +1033,12 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
       if (wide)
         LAUNCH("hash_search", s, dim3(grid_for(16 * G)), dim3(KBLOCK), k_hash_search<16>, G, (const uint8_t*)d_gmsg,
                (uint32_t)mlen, (const uint8_t*)d_gdom, 8, d_koff);
-      LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
-             (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr),
-             pl.tasks ? 1 : 0);
+      if (!wide && !pl.tasks)
+        LAUNCH_HASH(s, G, (const uint8_t*)d_gmsg, (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st);
+      else
+        LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
+               (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr),
+               pl.tasks ? 1 : 0);
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -2535,7 +2599,9 @@ size_t rb_ws_size(size_t n, size_t B) {
   s += align256(4 * ML_L_WORDS_PER_ITEM * ch_ml) + align256(ch_ml);                     // line products
   s += 2 * (align256(12 * FPW * nslots) + align256(nslots) + align256(nslots * sizeof(agg_chunk)));
   s += 2 * align256(nb) + align256(64);
-  s += align256(184 * n) + align256(4 * n) + align256(n) + verify_ws_size(n);           // the per-item fallback
+  // the per-item fallback over m <= n items (verify_nf(m) can exceed verify_nf(n) by the octet path's 2 per item)
+  const size_t oct = std::min<size_t>(n, BLS_ML_OCT_MAX_N);
+  s += align256(4 * n) + align256(n) + verify_ws_size(n) + align256(12 * FPW * 2 * oct) + align256(2 * oct);
   return s;
 }
 
@@ -2584,6 +2650,18 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
       LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
              (const uint32_t*)nullptr, 0);
     }
+    // BLS381_RB_HASH (measurement knob, order 0 only): 0 = the pair kernel k_hash_g2 in sequence;
+    // 1 = the one-lane candidate search + root (k_hash_cand_1) on the side stream beside
+    // decode_g1 (two one-lane launches of 2^16 items fill two waves per SIMD together), the
+    // cofactor map (k_hash_bp) in sequence
+    static const int rb_hash = env_knob("BLS381_RB_HASH", 0);
+    const bool hash_side = order != 1 && rb_hash == 1;
+    if (hash_side) {
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      LAUNCH("hash_cand", c->side, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
+      HIPC(hipEventRecord(c->ev_join3, c->side));
+    }
     LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
     // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
     LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
@@ -2602,9 +2680,13 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
-    if (order != 1)
+    if (hash_side) {
+      HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
+      LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
+    } else if (order != 1) {
       LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
              (const uint32_t*)nullptr, 0);
+    }
     LAUNCH("rb_scale_g1", sb, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
            (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
     if (order == 1) {
@@ -2658,19 +2740,22 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   if (stats) { stats[0] = n_batched; stats[1] = single.size(); stats[2] = n_failed; }
   const size_t m = single.size();
   if (m) {
+    // the per-item pairings over the points this call already decoded and hashed: the
+    // default pipeline minus its decodes and hash_to_G2 (the G2 test of the signatures is done)
     uint32_t* d_idx = b.take<uint32_t>(m);
-    uint8_t* gp = b.take<uint8_t>(48 * m);
-    uint8_t* gm = b.take<uint8_t>(32 * m);
-    uint8_t* gs = b.take<uint8_t>(96 * m);
-    uint8_t* gd = b.take<uint8_t>(8 * m);
     uint8_t* gv = b.take<uint8_t>(m);
-    void* vws = b.take<uint8_t>(verify_ws_size(m));
+    VerifyWs wm = carve_verify(b.take<uint8_t>(verify_ws_size(m)), m);
     HIPC(hipMemcpyAsync(d_idx, single.data(), 4 * m, hipMemcpyHostToDevice, s));
-    LAUNCH("gather_rows", s, dim3(grid_for(48 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, pks, 48u, gp);
-    LAUNCH("gather_rows", s, dim3(grid_for(32 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, msgs, 32u, gm);
-    LAUNCH("gather_rows", s, dim3(grid_for(96 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, sigs, 96u, gs);
-    LAUNCH("gather_rows", s, dim3(grid_for(8 * m)), blk, k_gather_rows, m, (const uint32_t*)d_idx, doms, 8u, gd);
-    if ((rc = run_verify_batch(c, m, gp, gm, gs, gd, gv, vws, s))) return rc;
+    const uint32_t rows = 2 * FP_LIMBS;
+    LAUNCH("gather_points", s, dim3(grid_for(rows * m)), blk, k_gather_soa, m, (const uint32_t*)d_idx,
+           (const uint32_t*)w.pk_aff, n, rows, 1u, wm.pk_aff);
+    LAUNCH("gather_points", s, dim3(grid_for(2 * rows * m)), blk, k_gather_soa, m, (const uint32_t*)d_idx,
+           (const uint32_t*)w.sig_aff, n, rows, 2u, wm.sig_aff);
+    LAUNCH("gather_points", s, dim3(grid_for(2 * rows * m)), blk, k_gather_soa, m, (const uint32_t*)d_idx,
+           (const uint32_t*)w.h_aff, n, rows, 2u, wm.h_aff);
+    LAUNCH("gather_status", s, dim3(grid_for(m)), blk, k_gather_st, m, (const uint32_t*)d_idx,
+           (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, wm.pk_st, wm.sig_st);
+    if ((rc = run_verify_pairings(m, wm, gv, s, false))) return rc;
     std::vector<uint8_t> h_gv(m);
     HIPC(hipMemcpyAsync(h_gv.data(), gv, m, hipMemcpyDeviceToHost, s));
     HIPC(hipStreamSynchronize(s));

@@ -766,6 +766,10 @@ BLS_HD inline fp_t fp_inv(const fp_t& am) {
     const uint64_t wb = ((uint64_t)b2 << 31) | ((uint64_t)b1 << 1) | (b0 >> 29);
     uint64_t xa = ((wa >> (bl - 1)) << 30) | (uint32_t)a[0];
     uint64_t xb = ((wb >> (bl - 1)) << 30) | (uint32_t)b[0];
+    if (t == 2 && bl <= 2) {   // n <= 62: the exact values (the paper's requirement for n <= 2k)
+      xa = (uint32_t)a[0] | ((uint64_t)(uint32_t)a[1] << 30) | ((uint64_t)(uint32_t)a[2] << 60);
+      xb = (uint32_t)b[0] | ((uint64_t)(uint32_t)b[1] << 30) | ((uint64_t)(uint32_t)b[2] << 60);
+    }
     int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
 #pragma unroll 10
     for (int j = 0; j < 30; ++j) {

@@ -201,6 +201,32 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_1(size_t n
   if (fin) soa_st_g2_1(out, n, i, h);
 }
 
+// hash_to_G2 in two launches (the throughput path): the try-and-increment search and the
+// square root on one lane per item (k_hash_cand_1: the root's two Fp exponentiations once
+// per item, where the pair form computes them on both lanes), then the cofactor map BP and
+// the affine conversion on lane pairs (k_hash_bp, in place over the candidate points).
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_cand_1(size_t n, const uint8_t* __restrict__ msgs,
+                                                       uint32_t mlen, const uint8_t* __restrict__ doms,
+                                                       int dom_stride, uint32_t* __restrict__ out) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  uint8_t dom[8];
+  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+  aff_t<fp2_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
+  soa_st_g2_1(out, n, i, c);
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_bp(size_t n, uint32_t* __restrict__ pts,
+                                                   uint8_t* __restrict__ st) {
+  const size_t i = item_index<2>();
+  if (i >= n) return;
+  const aff_t<fp2p_t> c = soa_ld_g2(pts, n, i);
+  aff_t<fp2p_t> h;
+  const bool fin = jac_to_aff(h, g2_mul_bp(c));
+  if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
+  if (fin) soa_st_g2(pts, n, i, h);
+}
+
 // The latency form of the try-and-increment search (bls_signature.md:74-86): W lanes per
 // message test candidates x + k, x + k + 1, ..., one Legendre symbol each (one-lane Fp2
 // arithmetic), and the item's lowest square offset is taken from a ballot; with W = 16 a

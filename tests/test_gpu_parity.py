@@ -812,12 +812,13 @@ def test_verify_multiple_batch_device_entry(native, golden, torsion):
     assert got == [int(e) for _, e in cases]
 
 
-def test_verify_multiple_grouped_device(native, golden, torsion):
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_verify_multiple_grouped_device(native, golden, torsion, policy):
     """bls381_verify_multiple_grouped_device (validate_indexed_attestation's
     verify_multiple-of-aggregates, aggregation fused): golden + torsion calls regrouped by
     message, with one group split in two under the same message (merged again) and an empty
-    group per call (the infinite aggregate); per-call verdicts == the fixtures' py_ecc column,
-    and committee batches == bls381_verify_multiple_batch."""
+    group per call (the infinite aggregate); per-call verdicts == the fixtures' column for the
+    subgroup policy (py_ecc's, or the strict one), directly and through the registry."""
     import ctypes
     import torch
     from bls381_amd import bls
@@ -829,7 +830,7 @@ def test_verify_multiple_grouped_device(native, golden, torsion):
     cases = [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
               c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
     cases += [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
-               c["expected_pyecc"]) for c in torsion["verify_multiple"]]
+               c["expected_" + policy]) for c in torsion["verify_multiple"]]
     rng = random.Random(0xB15_0C0D)
     sks = [rng.randrange(1, O.r) for _ in range(24)]
     pubs = [bls.privtopub(k) for k in sks]
@@ -879,17 +880,18 @@ def test_verify_multiple_grouped_device(native, golden, torsion):
                 d_doms.data_ptr(), d_v.data_ptr(), ws.data_ptr(), ctypes.c_void_p(stream.cuda_stream)))
         return [bool(x) for x in d_v.cpu().tolist()]
 
-    native.set_subgroup_policy("pyecc")
-    assert run(cases) == [bool(c[4]) for c in cases]
-    # one call per attestation, as an epoch: the same verdicts in a batch of 600 (task path)
-    many = [cases[i % len(cases)] for i in range(600)]
-    assert run(many) == [bool(c[4]) for c in many]
+    native.set_subgroup_policy(policy)
     from bls381_amd.registry import PubkeyRegistry
     reg = PubkeyRegistry(4096)
     try:
+        assert run(cases) == [bool(c[4]) for c in cases]
+        # one call per attestation, as an epoch: the same verdicts in a batch of 600 (task path)
+        many = [cases[i % len(cases)] for i in range(600)]
+        assert run(many) == [bool(c[4]) for c in many]
         assert run(cases, reg) == [bool(c[4]) for c in cases]
     finally:
         reg.close()
+        native.set_subgroup_policy("pyecc")
 
 
 # ------------------------------------ native multi-GPU ABI over RCCL
@@ -975,14 +977,17 @@ def test_randomized_batch_matches_per_item_verdicts(native, golden, torsion, pol
         native.set_subgroup_policy("pyecc")
 
 
-def test_randomized_batch_clean_and_tampered(native):
-    """4096 valid items: every sub-batch passes (no per-item re-verification); the same batch
-    with 1/16 tampered: identical verdicts to the default pipeline, failing sub-batches re-verified."""
+@pytest.mark.parametrize("n", [4096, 65536])
+def test_randomized_batch_clean_and_tampered(native, n):
+    """n valid items: every sub-batch passes (no per-item re-verification); the same batch
+    with 1/16 tampered: identical verdicts to the default pipeline, failing sub-batches
+    re-verified.  The re-verification runs the per-item pairings over the call's own decoded
+    points and hashes; at 2^16 items sub-batches of 64 (every one fails: 2^16 items, the split
+    Miller loop) and of 8 (~40 % fail: the quad loops) cover its layouts."""
     import ctypes
     import os as _os
     import torch
     L = native.lib()
-    n = 4096
     rng = np.random.default_rng(17)
     sk = 0xC0FFEE
     pk = O.privtopub(sk)
@@ -1014,5 +1019,6 @@ def test_randomized_batch_clean_and_tampered(native):
             sigs[96 * i:96 * i + 96] = sigs[96 * j:96 * j + 96]
     want = native.verify_batch(pk * n, msgs, bytes(sigs), doms)
     assert not want.all()
-    v, st = run(sigs, 64)
-    assert np.array_equal(v, want) and st[2] > 0 and st[0] + st[1] == n
+    for B in ((64, 8) if n > 4096 else (64,)):
+        v, st = run(sigs, B)
+        assert np.array_equal(v, want) and st[2] > 0 and st[0] + st[1] == n, B

@@ -339,6 +339,8 @@ def test_fp_inv_binary_gcd_edges(L):
     mont += [(1 << k) - 1 for k in range(2, 382)] + [(1 << k) + 1 for k in range(2, 381)]
     mont += list(range(1, 300)) + [q - k for k in range(1, 300)] + [q // 3, q // 5, (q - 1) // 2]
     mont += [rng.randrange(1, 1 << rng.randrange(2, 381)) for _ in range(3000)]
+    # common length <= 62 from the start (the exact-approximation branch, t == 2)
+    mont += [rng.randrange(1 << 59, 1 << 62) for _ in range(2000)] + [(1 << 61) | rng.getrandbits(60) for _ in range(500)]
     vals += [(m % q) * rinv % q for m in mont if m % q]
     vals += [rng.randrange(1, q) for _ in range(6000)]
     for a in vals:
