@@ -304,6 +304,41 @@ BLS_INLINE fp12_g<E> cyc_decompress(const cyc_bc<E>& g, const E& inv4g2) {
 // wave has one, the wave takes the Granger-Scott path instead (uniform branch).
 BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 
+// BLS_CYC_TAIL_GS=1: only the snapshots after 16, 48 and 57 squarings are compressed ones.
+// The last six squarings (runs 3, 2, 1) continue from the decompressed f^(2^57) with
+// Granger-Scott squarings on the full element: three decompressions and their shares of the
+// shared inversion (~30 Fp2 products) against six dearer squarings (~6 x 1.3 Fp2 products).
+#ifndef BLS_CYC_TAIL_GS
+#define BLS_CYC_TAIL_GS 1
+#endif
+
+#if BLS_CYC_TAIL_GS
+template <class E>
+BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+  cyc_bc<E> snap[3];
+  cyc_bc<E> g = cyc_compress(f);
+  bool zero = false;
+  for (int s = 0; s < 3; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cyc_csqr(g);
+    snap[s] = g;
+    const bool zs = fp2_is_zero(g.g2);   // evaluated on both lanes of a pair
+    zero = zero | zs;
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs(f);
+  const E d0 = fp2_mul_small(snap[0].g2, 4), d1 = fp2_mul_small(snap[1].g2, 4);
+  const E p01 = fp2_mul(d0, d1);
+  E inv = fp2_inv(fp2_mul(p01, fp2_mul_small(snap[2].g2, 4)));   // 1 / (d0 d1 d2)
+  fp12_g<E> x = cyc_decompress(snap[2], fp2_mul(inv, p01));       // f^(2^57)
+  inv = fp2_mul(inv, fp2_mul_small(snap[2].g2, 4));               // 1 / (d0 d1)
+  fp12_g<E> r = fp12_mul_inl(x, cyc_decompress(snap[1], fp2_mul(inv, d0)));
+  r = fp12_mul_inl(r, cyc_decompress(snap[0], fp2_mul(inv, d1)));
+  for (int s = 3; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) x = fp12_cyclotomic_sqr_inl(x);
+    r = fp12_mul_inl(r, x);
+  }
+  return fp12_conj(r);
+}
+#else
 template <class E>
 BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   cyc_bc<E> snap[6];
@@ -330,6 +365,7 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   }
   return fp12_conj(r);
 }
+#endif
 
 // f^(3 (q^12 - 1)/r).  3 is coprime to r, so the result is 1 exactly when the
 // reduced pairing value is 1 (DESIGN.md "Final exponentiation").
