@@ -111,7 +111,8 @@ def load_valu_peak():
 # profile key (bls381_profile_read) -> kernel symbol in rocprofv3 / PMC output
 PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2_1", "hash_to_g2": "k_hash_g2",
                   "miller_loop_2": "k_miller_verify", "final_exp": "k_final_exp_verdict",
-                  "miller_lines": "k_ml_lines", "miller_accum": "k_ml_accum"}
+                  "miller_lines": "k_ml_lines", "miller_accum": "k_ml_accum",
+                  "hash_cand": "k_hash_cand_1", "hash_bp": "k_hash_bp"}
 # the C2 batch (2^16 items) runs the split Miller loop: the monolithic count is not part of its pipeline
 PIPELINE_STAGES = ["decode_g1", "decode_g2", "hash_to_g2", "miller_lines", "miller_accum", "final_exp"]
 
