@@ -18,3 +18,6 @@ for P in "$P1" "$P2" "$P3" "$P4"; do
   timeout -k 10 600 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o p$i -- python3 tools/prof_workload.py $N > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $OUT/p$i.log; exit 1; }
   echo "pass $i ok"
 done
+# kernel durations of the same workload (kernel trace only; no counters in this run)
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 tools/prof_workload.py $N > $OUT/kt.log 2>&1 || { echo "kernel-trace pass failed"; tail -5 $OUT/kt.log; exit 1; }
+echo "kernel-trace pass ok"

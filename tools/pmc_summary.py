@@ -12,8 +12,23 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(k_[A-Za-z0-9_]+)", name)
-    return m.group(1) if m else name[:50]
+    """k_name, or k_name<args> for a template instance (demangled names; namespaces dropped)"""
+    m = re.search(r"(k_[A-Za-z0-9_]+)(<[^()]*>)?", name)
+    if not m:
+        return name[:50]
+    return m.group(1) + (re.sub(r"\s+|[A-Za-z0-9_]+::", "", m.group(2)) if m.group(2) else "")
+
+
+def kernel_ms(d):
+    """average kernel duration (ms) per kernel from a --kernel-trace --stats pass under d/kt, if present"""
+    tot = defaultdict(lambda: [0, 0.0])
+    for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                t = tot[short(row["Kernel_Name"])]
+                t[0] += 1
+                t[1] += (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6
+    return {k: v[1] / v[0] for k, v in tot.items() if v[0]}
 
 
 def main():
@@ -54,6 +69,12 @@ def main():
         "%.3f" % (data[k].get("SQ_WAIT_ANY", 0) / max(data[k].get("SQ_WAVE_CYCLES", 1), 1)) for k in kernels) + " |")
     lines.append("| HBM bytes (2*FETCH_KB*1024 + WRITE_KB*1024) | " + " | ".join(
         "%.4g" % (2 * data[k].get("FETCH_SIZE", 0) * 1024 + data[k].get("WRITE_SIZE", 0) * 1024) for k in kernels) + " |")
+    kms = kernel_ms(d)
+    if kms:
+        lines.append("| avg ms (kernel trace) | " + " | ".join("%.4g" % kms.get(k, float("nan")) for k in kernels) + " |")
+        lines.append("| HBM GB/s | " + " | ".join(
+            "%.4g" % ((2 * data[k].get("FETCH_SIZE", 0) * 1024 + data[k].get("WRITE_SIZE", 0) * 1024) /
+                      (kms[k] * 1e-3) / 1e9 if kms.get(k) else float("nan")) for k in kernels) + " |")
     out = "\n".join(lines)
     print(out)
     if len(sys.argv) > 2:
@@ -64,7 +85,8 @@ def main():
                   "fetch_kb": data[k].get("FETCH_SIZE"), "write_kb": data[k].get("WRITE_SIZE"),
                   "valu_insts": data[k].get("SQ_INSTS_VALU"), "valu_int64_insts": data[k].get("SQ_INSTS_VALU_INT64"),
                   "valu_int32_insts": data[k].get("SQ_INSTS_VALU_INT32"), "waves": data[k].get("SQ_WAVES"),
-                  "wait_any_frac": data[k].get("SQ_WAIT_ANY", 0) / max(data[k].get("SQ_WAVE_CYCLES", 1), 1)}
+                  "wait_any_frac": data[k].get("SQ_WAIT_ANY", 0) / max(data[k].get("SQ_WAVE_CYCLES", 1), 1),
+                  "avg_ms": kms.get(k)}
               for k in kernels}
         json.dump({"source": os.path.basename(os.path.normpath(d)), "workload": "tools/prof_workload.py",
                    "kernels": js}, open(os.path.splitext(sys.argv[2])[0] + ".json", "w"), indent=1)

@@ -49,6 +49,23 @@ def main():
                                                              aws.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
     torch.cuda.synchronize()
     assert int(d_st.abs().sum().item()) == 0
+    # the same committees from the device pubkey registry (validator indices): k_agg_chunks<fp_t,1> reads
+    # decoded SoA limbs by index and has no scratch frame -- its HBM bytes against the algorithmic
+    # 112 B + 4 B per member show whether the limb loads are coalesced
+    from bls381_amd.registry import PubkeyRegistry
+    ref = d_out.clone()
+    reg = PubkeyRegistry(n)
+    ent = reg.add([pks[48 * i:48 * i + 48] for i in range(n)])
+    d_idx = t(ent[idx].astype(np.uint32).tobytes())
+    d_out.zero_()
+    rws = torch.empty(L.bls381_registry_aggregate_workspace_size(nc, nc * cs), dtype=torch.uint8, device=dev)
+    for _ in range(2):
+        native.check(L.bls381_registry_aggregate_indices_device(
+            reg._h, nc, off.ctypes.data_as(ctypes.c_void_p), nc * cs, d_idx.data_ptr(), d_out.data_ptr(),
+            d_st.data_ptr(), rws.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    torch.cuda.synchronize()
+    assert torch.equal(d_out, ref) and int(d_st.abs().sum().item()) == 0
+    reg.close()
     print("prof workload ok", n)
 
 
