@@ -12,7 +12,7 @@ the same error behaviour as the py_ecc 1.7.0 calls they replace
 * bls_aggregate_* raise ValueError on an invalid point encoding;
 * a domain outside [0, 2^64) raises OverflowError (int.to_bytes).
 
-Divergences from that contract (each tested in tests/test_abi_and_shim.py):
+Divergences from that contract (tested in tests/test_gpu_parity.py):
 * a message longer than _native.MSG_MAX (1 MiB) raises ValueError from bls_verify,
   bls_verify_multiple and bls_sign, where py_ecc would hash it and return a verdict.
   The spec's message_hash is Bytes32, so no spec call reaches the limit; raising
