@@ -825,11 +825,35 @@ template <> struct pt_traits<fp2p_t> {
   __device__ static bool in_subgroup(const aff_t<fp2p_t>& a) { return g2_in_subgroup(a); }
 };
 
-template <class F> __device__ aff_t<F> reg_ld_aff(const uint32_t* aff, size_t cap, size_t r);
-template <> __device__ __forceinline__ aff_t<fp_t> reg_ld_aff<fp_t>(const uint32_t* aff, size_t cap, size_t r) {
-  return soa_ld_g1(aff, cap, r);
+// Registry points are entry-major (AoS): entry r's affine x and y limbs are the 28
+// consecutive words at aff + 28 r (112 B, 16-byte aligned).  Members are read by
+// validator index, i.e. at random entries: an entry is one contiguous 112-byte read
+// (seven 16-byte loads) instead of 28 limb loads that each touch their own cache line,
+// as a limb-major (SoA) layout would give for a random index.
+constexpr int REG_WORDS = 2 * FP_LIMBS;
+__device__ __forceinline__ void reg_st_g1(uint32_t* aff, size_t r, const aff_t<fp_t>& a) {
+  uint4* p = reinterpret_cast<uint4*>(aff + (size_t)REG_WORDS * r);
+  uint32_t w[REG_WORDS];
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) { w[k] = a.x.w[k]; w[FP_LIMBS + k] = a.y.w[k]; }
+#pragma unroll
+  for (int q = 0; q < REG_WORDS / 4; ++q) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
-template <> __device__ __forceinline__ aff_t<fp2p_t> reg_ld_aff<fp2p_t>(const uint32_t*, size_t, size_t) {
+template <class F> __device__ aff_t<F> reg_ld_aff(const uint32_t* aff, size_t r);
+template <> __device__ __forceinline__ aff_t<fp_t> reg_ld_aff<fp_t>(const uint32_t* aff, size_t r) {
+  const uint4* p = reinterpret_cast<const uint4*>(aff + (size_t)REG_WORDS * r);
+  uint32_t w[REG_WORDS];
+#pragma unroll
+  for (int q = 0; q < REG_WORDS / 4; ++q) {
+    const uint4 v = p[q];
+    w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+  }
+  aff_t<fp_t> a;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) { a.x.w[k] = w[k]; a.y.w[k] = w[FP_LIMBS + k]; }
+  return a;
+}
+template <> __device__ __forceinline__ aff_t<fp2p_t> reg_ld_aff<fp2p_t>(const uint32_t*, size_t) {
   __builtin_trap();   // the registry holds G1 pubkeys only; never instantiated with entries
 }
 
@@ -839,9 +863,9 @@ template <> __device__ __forceinline__ aff_t<fp2p_t> reg_ld_aff<fp2p_t>(const ui
 enum : int { AGG_BYTES = 0, AGG_JAC = 1, AGG_REGISTRY = 2 };
 struct agg_reg_src {
   const int32_t* entry;   // per input: registry entry or -1
-  const uint32_t* aff;    // registry SoA affine points (stride cap)
+  const uint32_t* aff;    // registry affine points, entry-major (reg_ld_aff)
   const uint8_t* st;      // registry entry status: ST_OK / ST_INF / ST_BAD
-  size_t cap;             // SoA stride
+  size_t cap;             // entries allocated
   size_t size;            // entries in use: an entry >= size is an error (BAD), never read
 };
 
@@ -858,7 +882,7 @@ __device__ __forceinline__ void agg_accumulate(jac_t<F>& acc, bool& bad, uint32_
       if (rs == ST_BAD) {
         bad = true;
       } else if (rs == ST_OK) {
-        const aff_t<F> a = reg_ld_aff<F>(reg.aff, reg.cap, (size_t)r);
+        const aff_t<F> a = reg_ld_aff<F>(reg.aff, (size_t)r);
         if (check && !pt_traits<F>::in_subgroup(a)) bad = true;
         else acc = jac_add_aff(acc, a);
       }
@@ -976,7 +1000,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g1_affine(size
 
 // -------------------------------------------------------- pubkey registry --
 // Device-resident registry of decoded pubkeys: entry j
-// holds the 48-byte key, its status and its affine point (SoA, stride cap); an
+// holds the 48-byte key, its status and its affine point (entry-major, reg_st_g1); an
 // open-addressing table (u32 entry per slot, REG_EMPTY when free, linear
 // probing, power-of-two size) maps key bytes to entries.
 constexpr uint32_t REG_EMPTY = 0xFFFFFFFFu;
@@ -1007,7 +1031,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_reg_decode(size_t 
   const size_t j = first + t;
   aff_t<fp_t> a;
   const int s = g1_decompress(a, keys + 48 * j);
-  if (s == PT_OK) soa_st_g1(aff, cap, j, a);
+  if (s == PT_OK) reg_st_g1(aff, j, a);
   st[j] = s == PT_OK ? ST_OK : (s == PT_INF ? ST_INF : ST_BAD);
 }
 
