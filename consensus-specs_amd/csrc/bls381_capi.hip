@@ -344,17 +344,23 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // Decode waves fill the SIMD slots that finished hash waves free (measured in DESIGN.md §10).
   // BLS381_C2_ORDER (measurement knob): 1 = the decodes on the side stream beside hash_to_G2,
   // 0 = everything in sequence on the main stream
-  static const int c2_order = env_knob("BLS381_C2_ORDER", 1);
+  // 2 = as 1 with decode_g2 before decode_g1; 3 (default) = as 1, and the split hash's
+  // cofactor launch (k_hash_bp) waits for both decodes instead of sharing the chip with
+  // them: the one-lane search + root (k_hash_cand_1) pairs with the one-lane decodes, the
+  // full-chip k_hash_bp then runs alone.  r03v, one box, two runs each: order 1 2.137 /
+  // 2.152 M/s (k_hash_bp 4.9-5.0 ms beside decode_g2), order 3 2.199 / 2.201 (3.4 ms)
+  static const int c2_order = env_knob("BLS381_C2_ORDER", 3);
   hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+  if (c2_order != 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
 #if BLS_DECODE_G2_SIDE
   // both decodes in sequence beside hash_to_G2
   if (g2_one_lane() & 1)
     LAUNCH("decode_g2", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
   else
     LAUNCH("decode_g2", sd, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
+  if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
   HIPC(hipEventRecord(c->ev_join, c->side));
@@ -367,7 +373,11 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
   if (!wide && (g2_one_lane() & 2))
     LAUNCH("hash_to_g2", s, g, b, k_hash_g2_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
-  else if (!wide)
+  else if (!wide && c2_order == 3 && hash_split()) {
+    LAUNCH("hash_cand", s, g, b, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
+    HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    LAUNCH("hash_bp", s, g2, b, k_hash_bp, n, w.h_aff, (uint8_t*)nullptr);
+  } else if (!wide)
     LAUNCH_HASH(s, n, msgs, 32u, doms, 8, w.h_aff, (uint8_t*)nullptr);
   else
     LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
@@ -2654,6 +2664,7 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     // 1 = the one-lane candidate search + root (k_hash_cand_1) on the side stream beside
     // decode_g1 (two one-lane launches of 2^16 items fill two waves per SIMD together), the
     // cofactor map (k_hash_bp) in sequence
+    // 2 = the split hash (k_hash_cand_1, k_hash_bp) in sequence where the pair kernel runs
     static const int rb_hash = env_knob("BLS381_RB_HASH", 0);
     const bool hash_side = order != 1 && rb_hash == 1;
     if (hash_side) {
@@ -2682,6 +2693,9 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     HIPC(hipEventRecord(c->ev_join2, c->prio));
     if (hash_side) {
       HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
+      LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
+    } else if (order != 1 && rb_hash == 2) {
+      LAUNCH("hash_cand", s, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
       LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
     } else if (order != 1) {
       LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,

@@ -205,16 +205,105 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_1(size_t n
 // square root on one lane per item (k_hash_cand_1: the root's two Fp exponentiations once
 // per item, where the pair form computes them on both lanes), then the cofactor map BP and
 // the affine conversion on lane pairs (k_hash_bp, in place over the candidate points).
+//
+// BLS_HASH_COMPACT=1: the try-and-increment search runs over the whole wave as a pool.
+// A lane-per-item loop runs until the wave's slowest item has found its square (~7 rounds
+// for 64 items at success probability 1/2, against a mean of 2).  Here, each round,
+// the wave's unresolved items share all 64 lanes: with m items left, item t (the r-th
+// unresolved) takes the lanes j = r, r + m, r + 2m, ... and tests its offsets k_t, k_t + 1,
+// ... one per lane; its square is the lowest successful offset (the spec's candidate
+// order), else k_t advances past all of them.  ~3 rounds per wave.
+#ifndef BLS_HASH_COMPACT
+#define BLS_HASH_COMPACT 1
+#endif
+
+// the r-th set bit (r < popcount(m)) of a 64-bit mask
+__device__ __forceinline__ uint32_t nth_set_bit64(uint64_t m, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lo = m & ((w == 64 ? ~0ull : (1ull << w)) - 1ull);
+    const uint32_t c = (uint32_t)__builtin_popcountll(lo);
+    if (r >= c) { r -= c; m >>= w; pos += w; }
+    else m = lo;
+  }
+  return pos;
+}
+
+__device__ __forceinline__ uint32_t lane_shfl(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
+
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_cand_1(size_t n, const uint8_t* __restrict__ msgs,
                                                        uint32_t mlen, const uint8_t* __restrict__ doms,
                                                        int dom_stride, uint32_t* __restrict__ out) {
   const size_t i = item_index<1>();
+#if BLS_HASH_COMPACT
+  // every lane of the wave takes part in the pooled search: no early return before it
+  const bool valid = i < n;
+  fp2_t x;
+  if (valid) {
+    uint8_t dom[8];
+    ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+    const uint8_t* msg = msgs + (size_t)mlen * i;
+    uint32_t d[8];
+    sha256_msg_dom_tag(d, msg, mlen, dom, 1);
+    x.c0 = fp_to_mont(fp_plain_from_digest(d));
+    sha256_msg_dom_tag(d, msg, mlen, dom, 2);
+    x.c1 = fp_to_mont(fp_plain_from_digest(d));
+  } else {
+    x.c0 = fp_zero(); x.c1 = fp_zero();
+  }
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t k = 0;            // this lane's item: next offset to test
+  int32_t found = valid ? -1 : 0;
+  while (true) {
+    const uint64_t P = __builtin_amdgcn_ballot_w64(found < 0);
+    if (P == 0) break;
+    const uint32_t m = (uint32_t)__builtin_popcountll(P);
+    const uint32_t t = nth_set_bit64(P, lane % m);        // the item this lane tests for
+    const uint32_t off = lane_shfl(k, t) + lane / m;
+    fp2_t y;
+#pragma unroll
+    for (int w = 0; w < FP_LIMBS; ++w) { y.c0.w[w] = lane_shfl(x.c0.w[w], t); y.c1.w[w] = lane_shfl(x.c1.w[w], t); }
+    fp_t o = fp_zero();
+    o.w[0] = off;
+    y.c0 = fp_add(y.c0, fp_to_mont(o));
+    const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(y), y), G2_B_M);
+    const bool sq = fp_legendre(fp_add(fp_sqr(rhs.c0), fp_sqr(rhs.c1))) >= 0;
+    const uint64_t B = __builtin_amdgcn_ballot_w64(sq);
+    if (found < 0) {
+      // this lane owns an unresolved item: its lanes are r, r + m, ... (r = its rank in P)
+      const uint32_t r = (uint32_t)__builtin_popcountll(P & ((1ull << lane) - 1ull));
+      int32_t first = -1;
+      uint32_t cnt = 0;
+      for (uint32_t j = r; j < 64; j += m, ++cnt)
+        if (first < 0 && ((B >> j) & 1ull)) first = (int32_t)cnt;
+      if (first >= 0) found = (int32_t)(k + (uint32_t)first);
+      else k += cnt;
+    }
+  }
+  if (!valid) return;
+  {
+    fp_t o = fp_zero();
+    o.w[0] = (uint32_t)found;
+    x.c0 = fp_add(x.c0, fp_to_mont(o));
+  }
+  const fp2_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), G2_B_M);
+  fp2_t y;
+  fp2_sqrt(y, rhs);   // succeeds: rhs is a square
+  aff_t<fp2_t> c;
+  c.x = x;
+  c.y = g2_select_root(y);
+  soa_st_g2_1(out, n, i, c);
+#else
   if (i >= n) return;
   uint8_t dom[8];
   ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
   aff_t<fp2_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   soa_st_g2_1(out, n, i, c);
+#endif
 }
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_bp(size_t n, uint32_t* __restrict__ pts,
                                                    uint8_t* __restrict__ st) {
