@@ -212,8 +212,20 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
 #ifndef BLS_FE_QUAD_MAX_N
 #define BLS_FE_QUAD_MAX_N 49152
 #endif
+// final exponentiations of at most this many values run on lane octets (k_final_exp_verdict_o:
+// the squarings split four ways) -- BLS381_FE_OCT=0 keeps them on quads (measurement knob)
+#ifndef BLS_FE_OCT_MAX_N
+#define BLS_FE_OCT_MAX_N 8192
+#endif
+int env_knob(const char* name, int def);
+bool fe_oct(size_t n) {
+  static const int on = env_knob("BLS381_FE_OCT", 0);
+  return on && n <= BLS_FE_OCT_MAX_N;
+}
 int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts) {
-  if (n <= BLS_FE_QUAD_MAX_N)
+  if (fe_oct(n))
+    LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_o<1>, n, f, st, verdicts);
+  else if (n <= BLS_FE_QUAD_MAX_N)
     LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), dim3(KBLOCK), k_final_exp_verdict_q<1>, n, f, st, verdicts);
   else
     LAUNCH("final_exp", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_final_exp_verdict, n, f, st, verdicts);
@@ -396,8 +408,12 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
     LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
            (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
            w.f, w.f_st);
-    LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), b, k_final_exp_verdict_q<2>, n, (const uint32_t*)w.f,
-           (const uint8_t*)w.f_st, verdicts);
+    if (fe_oct(n))
+      LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), b, k_final_exp_verdict_o<2>, n, (const uint32_t*)w.f,
+             (const uint8_t*)w.f_st, verdicts);
+    else
+      LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), b, k_final_exp_verdict_q<2>, n, (const uint32_t*)w.f,
+             (const uint8_t*)w.f_st, verdicts);
     return 0;
   }
   if (n <= BLS_ML_QUAD_MAX_N) {

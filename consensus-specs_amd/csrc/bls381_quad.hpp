@@ -464,4 +464,118 @@ __device__ inline fq12_t final_exp_q(const fq12_t& f) {
   return fq12_mul(c, t3);
 }
 
+// ------------------------------------- compressed squarings on a lane octet --
+// The lowest-latency form of cyc_exp_x for single calls: an item's FE runs on 8 lanes,
+// two quads holding the same fq12_t (every Fp12 step is computed on both, identically),
+// and only the 63 Karabina squarings per x-power -- most of the FE -- are split four ways:
+// each lane pair of the octet holds one of (g4, g2, g5, g3) (pairs 0..3) and computes that
+// coefficient's update as ONE lazily reduced sum of three products,
+//   pair 0  g4' = 3 (g2^2 + xi g3^2) - 2 g4     pair 1  g2' = 6 xi g4 g5 + 2 g2
+//   pair 2  g5' = 6 g2 g3 + 2 g5                pair 3  g3' = 3 (g4^2 + xi g5^2) - 2 g3
+// (the product outputs leave their third product zero, so every lane runs the same
+// instruction stream): 3 half-products and 1 reduction per lane per squaring, against 5
+// and 2 on a quad.  The two operands come from the same quad's other pair (DPP quad_perm)
+// and the other quad (DPP row_shl/row_shr by 4).
+__device__ __forceinline__ bool od_upper() { return (threadIdx.x & 4u) != 0; }
+// the same lane of the other quad of the octet
+__device__ __forceinline__ fp_t od_cross(const fp_t& a) {
+  return fp_sel(od_upper(), pr_dpp<0x114>(a), pr_dpp<0x104>(a));   // row_shr:4 | row_shl:4
+}
+// quad compressed value (both quads equal) -> this pair's coefficient: lower quad x, upper y
+__device__ __forceinline__ fp2p_t co_enter(const cq_t& g) { return qd_sel(od_upper(), g.y, g.x); }
+__device__ __forceinline__ cq_t co_exit(const fp2p_t& s) {
+  const bool up = od_upper();
+  const fp2p_t o = pr_make(od_cross(s.v));
+  cq_t g;
+  g.x = qd_sel(up, o, s);
+  g.y = qd_sel(up, s, o);
+  return g;
+}
+
+__device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
+  const bool up = od_upper(), p = pr_odd();
+  const uint32_t pair = (threadIdx.x >> 1) & 3u;
+  const bool sq = pair == 0 || pair == 3, xp = pair == 1;
+  const fp_t a = pr_dpp<DPP_HSWAP>(g.v);
+  const fp_t b = pr_dpp<DPP_HSWAP>(od_cross(g.v));
+  const fp_t X = fp_sel(up, b, a), Y = fp_sel(up, a, b);     // (g2, g3) or (g4, g5)
+  const fp_t X0 = pr_dpp<DPP_EVEN>(X), X1 = pr_dpp<DPP_ODD>(X);
+  const fp_t Y0 = pr_dpp<DPP_EVEN>(Y), Y1 = pr_dpp<DPP_ODD>(Y);
+  lv_t u;
+  {
+    uint32_t us[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) us[k] = Y0.w[k] + (p ? Y1.w[k] : Q2B_LIMBS[k] - Y1.w[k]);
+    lv_from(u, fp_reduce_lc<2>(us));   // Y0 -+ Y1 reduced (the square's operand)
+  }
+  lv_t a1, b1, a2, b2, a3, b3;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int32_t x0 = (int32_t)X0.w[k], x1 = (int32_t)X1.w[k], y0 = (int32_t)Y0.w[k], y1 = (int32_t)Y1.w[k];
+    const int32_t ys = y0 + y1, yd = y0 - y1;
+    // SQ:    Re (x0+x1)(x0-x1) + u^2 - 2 y1^2,  Im 2 x0 x1 + u^2 - 2 y1^2   (lz_sqr_xisqr)
+    // XPROD: Re x0 (y0-y1) - x1 (y0+y1),        Im x0 (y0+y1) + x1 (y0-y1) (lz_xi_mul)
+    // PROD:  Re x0 y0 - x1 y1,                  Im x0 y1 + x1 y0           (lz_mul)
+    a1[k] = sq ? (p ? 2 * x0 : x0 + x1) : x0;
+    b1[k] = sq ? (p ? x1 : x0 - x1) : (xp ? (p ? ys : yd) : (p ? y1 : y0));
+    a2[k] = sq ? u[k] : x1;
+    b2[k] = sq ? u[k] : (xp ? (p ? yd : -ys) : (p ? y0 : -y1));
+    a3[k] = sq ? -2 * y1 : 0;
+    b3[k] = sq ? y1 : 0;
+  }
+  // columns: 3 x 14 products < 2^57 (< 2^62.4) plus the reduction's < 2^59.8; values in
+  // (-16 q^2, 12 q^2) as for lz_sqr_xisqr (the product outputs: |X| < 16 q^2)
+  wide_t T;
+  wz_init(T);
+  wmac(T, a1, b1);
+  wmac(T, a2, b2);
+  wmac(T, a3, b3);
+  const fp_t R = wredc(T);
+  return pr_make(fp_6p2_3m2(!sq, R, R, g.v));
+}
+
+// cyc_exp_x_q with the squarings on the octet
+__device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t& f) {
+  const bool hi = qd_hi();
+  cq_t snap[6];
+  fp2p_t g = co_enter(cq_compress(f));
+  bool zero = false;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = co_sqr(g);
+    snap[s] = co_exit(g);
+    zero = zero | fp2_is_zero(cq_g2(snap[s]));
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs_q(f);
+  fp2p_t pre[6];
+  pre[0] = fp2_mul_small(cq_g2(snap[0]), 4);
+  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(cq_g2(snap[s]), 4));
+  fp2p_t inv = fp2_inv(pre[5]);
+  fq12_t r;
+  for (int s = 5; s >= 0; --s) {
+    fp2p_t is = inv;
+    if (s) {
+      const fp2p_t p = fp2_mul(inv, qd_sel(hi, fp2_mul_small(cq_g2(snap[s]), 4), pre[s - 1]));
+      const fp2p_t po = qd_swap(p);
+      is = qd_sel(hi, po, p);
+      inv = qd_sel(hi, p, po);
+    }
+    const fq12_t x = cq_decompress(snap[s], is);
+    r = (s == 5) ? x : fq12_mul(r, x);
+  }
+  return fq12_conj(r);
+}
+
+// final_exp_q with cyc_exp_x_o: both quads of the octet hold f
+__device__ inline fq12_t final_exp_o(const fq12_t& f) {
+  fq12_t t = fq12_mul(fq12_conj(f), fq12_inv(f));
+  t = fq12_mul(fq12_frob(t, 2), t);
+  fq12_t a = fq12_mul(cyc_exp_x_o(t), fq12_conj(t));
+  a = fq12_mul(cyc_exp_x_o(a), fq12_conj(a));
+  const fq12_t b = fq12_mul(cyc_exp_x_o(a), fq12_frob(a, 1));
+  const fq12_t bx2 = cyc_exp_x_o(cyc_exp_x_o(b));
+  const fq12_t c = fq12_mul(fq12_mul(bx2, fq12_frob(b, 2)), fq12_conj(b));
+  const fq12_t t3 = fq12_mul(fq12_sqr(t), t);
+  return fq12_mul(c, t3);
+}
+
 }  // namespace bls381

@@ -7,6 +7,7 @@ restatement).  Larger sizes are covered by size-independent properties
 """
 import os
 import random
+import sys
 
 import numpy as np
 import pytest
@@ -1022,3 +1023,47 @@ def test_randomized_batch_clean_and_tampered(native, n):
     for B in ((64, 8) if n > 4096 else (64,)):
         v, st = run(sigs, B)
         assert np.array_equal(v, want) and st[2] > 0 and st[0] + st[1] == n, B
+
+
+# ---------------------------- octet-layout final exponentiation (latency knob)
+_OCT_SCRIPT = r"""
+import json, os, sys
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "consensus-specs_amd")]
+import numpy as np
+from bls381_amd import _native as native
+native.init(0)
+gb = json.load(open(os.path.join(root, "tests", "golden", "bls_golden_batches.json")))
+tor = json.load(open(os.path.join(root, "tests", "golden", "bls_torsion.json")))
+items = [(c, c["expected"]) for c in gb["verify"] if len(bytes.fromhex(c["message"])) == 32]
+items += [(c, c["expected_pyecc"]) for c in tor["verify"]]
+for n in (len(items), 3000):
+    sel = [items[i % len(items)] for i in range(n)]
+    got = native.verify_batch(b"".join(bytes.fromhex(c["pubkey"]) for c, _ in sel),
+                              b"".join(bytes.fromhex(c["message"]) for c, _ in sel),
+                              b"".join(bytes.fromhex(c["signature"]) for c, _ in sel),
+                              b"".join(int(c["domain"]).to_bytes(8, "big") for c, _ in sel))
+    assert list(got) == [e for _, e in sel], n
+vms = [(c, c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+vms += [(c, c["expected_pyecc"]) for c in tor["verify_multiple"]]
+off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
+for c, _ in vms:
+    pks += b"".join(bytes.fromhex(p) for p in c["pubkeys"]); msgs += b"".join(bytes.fromhex(m) for m in c["messages"])
+    sigs += bytes.fromhex(c["signature"]); doms += int(c["domain"]).to_bytes(8, "big")
+    off.append(off[-1] + len(c["pubkeys"]))
+assert list(native.verify_multiple_batch(np.array(off, dtype=np.uint32), pks, msgs, 32, sigs, doms)) == [e for _, e in vms]
+print("octet fe ok")
+"""
+
+
+def test_octet_final_exponentiation_knob():
+    """BLS381_FE_OCT=1 (read once per process, so in a child process): the octet-layout
+    final exponentiation (k_final_exp_verdict_o, squarings split over four lane pairs) gives
+    the fixture verdicts for bls_verify batches (one and two values per item) and
+    verify_multiple batches."""
+    import subprocess
+    env = dict(os.environ, BLS381_FE_OCT="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _OCT_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "octet fe ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
