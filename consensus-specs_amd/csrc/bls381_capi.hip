@@ -360,8 +360,12 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // cofactor launch (k_hash_bp) waits for both decodes instead of sharing the chip with
   // them: the one-lane search + root (k_hash_cand_1) pairs with the one-lane decodes, the
   // full-chip k_hash_bp then runs alone.  r03v, one box, two runs each: order 1 2.137 /
-  // 2.152 M/s (k_hash_bp 4.9-5.0 ms beside decode_g2), order 3 2.199 / 2.201 (3.4 ms)
-  static const int c2_order = env_knob("BLS381_C2_ORDER", 3);
+  // 2.152 M/s (k_hash_bp 4.9-5.0 ms beside decode_g2), order 3 2.199 / 2.201 (3.4 ms).
+  // Under the strict policy decode_g1 carries the G1 subgroup test (3.6 ms), and waiting for
+  // it costs more than sharing the chip: order 1 2.111 / 2.113 against order 3 2.062 / 2.051
+  // (r03y).  Default: 3 for py_ecc, 1 for strict.
+  static const int c2_order_env = env_knob("BLS381_C2_ORDER", -1);
+  const int c2_order = c2_order_env >= 0 ? c2_order_env : (chk ? 1 : 3);
   hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
