@@ -222,7 +222,7 @@ __device__ __forceinline__ uint32_t nth_set_bit64(uint64_t m, uint32_t r) {
   uint32_t pos = 0;
 #pragma unroll
   for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t lo = m & ((w == 64 ? ~0ull : (1ull << w)) - 1ull);
+    const uint64_t lo = m & ((1ull << w) - 1ull);
     const uint32_t c = (uint32_t)__builtin_popcountll(lo);
     if (r >= c) { r -= c; m >>= w; pos += w; }
     else m = lo;
