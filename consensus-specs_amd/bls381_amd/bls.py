@@ -23,15 +23,16 @@ exponentiation decides the call).
 
 Two switches mirror behaviour the reference leaves to py_ecc:
 * DOMAIN_BYTEORDER -- how the int domain becomes 8 bytes (SURVEY.md A.2);
-* SUBGROUP_POLICY  -- "pyecc" (default): py_ecc 1.7.0's subgroup behaviour -- no
-  subgroup test, only the on-curve test; "strict": every pubkey / signature must
-  also lie in G1 / G2 (specs/bls_signature.md:135-136,143-144).  The verdicts
-  differ only on points with a small-order component (tests/golden/bls_torsion.json
-  has both columns).  Under either policy *decoding* is the spec's strict codec
-  (bls_signature.md:47-52,58-64: c_flag set, x < q, canonical infinity); py_ecc
-  1.7.0 may accept some non-canonical encodings that this rejects,
-  so "pyecc" names the subgroup behaviour, not the codec.
-  The switch applies to this module's calls only: each verify runs inside a
+* SUBGROUP_POLICY  -- "pyecc" (default): py_ecc 1.7.0's behaviour -- its lax codec
+  (b_flag set means infinity whatever the other bits, x taken mod
+  2^381 and reduced mod q, no c_flag or x < q check) and no subgroup test, only the
+  on-curve test; "strict": the spec's codec (bls_signature.md:47-52,58-64: c_flag
+  set, x < q, canonical infinity) and every pubkey / signature must also lie in
+  G1 / G2 (:135-136,143-144).  The verdicts and aggregate bytes differ only on
+  points with a small-order component (tests/golden/bls_torsion.json) and on
+  non-canonical encodings (tests/golden/bls_noncanonical.json); both files carry
+  both columns.
+  The switch applies to this module's calls only: each call runs inside a
   thread-local policy scope (_native.subgroup_policy_scope), so the process-wide
   policy other front ends read (_native.set_subgroup_policy) is never rewritten.
 """
@@ -47,8 +48,8 @@ STUB_PUBKEY = b'\x22' * 48
 # py_ecc 1.7.0 serialises the int domain big-endian; one switch.
 DOMAIN_BYTEORDER = "big"
 
-# Subgroup checks on the verify paths: "pyecc" (py_ecc 1.7.0, the reference's
-# behaviour) or "strict" (the spec's valid-G1/G2-point rule).  One switch.
+# Codec and subgroup checks: "pyecc" (py_ecc 1.7.0, the reference's behaviour) or
+# "strict" (the spec's point format and valid-G1/G2-point rule).  One switch.
 SUBGROUP_POLICY = "pyecc"
 
 
@@ -157,9 +158,10 @@ def bls_aggregate_pubkeys(pubkeys):
     pks = [bytes(p) for p in pubkeys]
     if any(len(p) != 48 for p in pks):
         raise ValueError("pubkeys must be 48 bytes")
-    if _pubkey_registry is not None:
-        return _pubkey_registry.aggregate_pubkeys(pks)
-    return _native.aggregate_pubkeys(b"".join(pks))
+    with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+        if _pubkey_registry is not None:
+            return _pubkey_registry.aggregate_pubkeys(pks)
+        return _native.aggregate_pubkeys(b"".join(pks))
 
 
 @only_with_bls(alt_return=STUB_SIGNATURE)
@@ -167,7 +169,8 @@ def bls_aggregate_signatures(signatures):
     sigs = [bytes(s) for s in signatures]
     if any(len(s) != 96 for s in sigs):
         raise ValueError("signatures must be 96 bytes")
-    return _native.aggregate_signatures(b"".join(sigs))
+    with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+        return _native.aggregate_signatures(b"".join(sigs))
 
 
 @only_with_bls(alt_return=STUB_SIGNATURE)

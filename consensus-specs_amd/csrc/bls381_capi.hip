@@ -40,6 +40,10 @@ std::atomic<int> g_policy{BLS381_POLICY_PYECC};
 thread_local int t_policy = -1;
 int current_policy() { return t_policy >= 0 ? t_policy : g_policy.load(std::memory_order_relaxed); }
 int check_subgroups() { return current_policy() == BLS381_POLICY_STRICT ? 1 : 0; }
+// decode / aggregation kernel flags (bls381_kernels.hpp CHK_*) for subgroup mode `sub`
+// under the current policy: the py_ecc policy decodes with py_ecc 1.7.0's lax codec
+// (SURVEY.md A.4), the strict policy with the spec's (bls_signature.md:47-52,58-64)
+int policy_flags(int sub) { return sub | (current_policy() == BLS381_POLICY_PYECC ? CHK_LAX : 0); }
 
 // Host memory that an async copy still reads: released once an event
 // recorded after the copy has completed (device-pointer entry points return
@@ -369,18 +373,18 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  if (c2_order != 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+  if (c2_order != 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
 #if BLS_DECODE_G2_SIDE
   // both decodes in sequence beside hash_to_G2
   if (g2_one_lane() & 1)
-    LAUNCH("decode_g2", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
+    LAUNCH("decode_g2", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
   else
-    LAUNCH("decode_g2", sd, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
-  if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    LAUNCH("decode_g2", sd, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
+  if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
   HIPC(hipEventRecord(c->ev_join, c->side));
-  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, sig_in_loop ? 0 : chk);
+  LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
 #endif
   // small batches: the wide search first (16 candidates per message in one round), so the
   // hash does not wait for the batch's slowest sequential search
@@ -1035,7 +1039,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
       agg_reg_src rs{};
       if (reg) { rs = *reg; rs.entry = (const int32_t*)d_gpks; }
       int rc = run_agg<fp_t>(pl.agg, G, reg ? nullptr : d_gpks, sub, side, &jac, &bad, &used, b.left(),
-                             reg ? &rs : nullptr, chk);
+                             reg ? &rs : nullptr, policy_flags(chk));
       if (rc) return rc;
       b.off += used;
       LAUNCH("agg_g1_affine", side, dim3(grid_for(G)), dim3(KBLOCK), k_agg_g1_affine, G, jac, bad, agg_aff, agg_st);
@@ -1046,7 +1050,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     // outlast it
     HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
     LAUNCH("decode_g2", c->side2, dim3(grid_for(2 * ncalls)), dim3(KBLOCK), k_decode_g2, ncalls, d_sigs, sig_aff,
-           sig_st, chk);
+           sig_st, policy_flags(chk));
     if (!pl.tasks) {
       // large batches: the signature pairs run here, beside hash_to_G2, so the group pairs fill
       // whole quads and the main Miller launch has no partial last round of waves
@@ -1495,8 +1499,10 @@ int bls381_final_verify(size_t k, const uint8_t* parts576) try {
 }
 
 // ---- aggregation
+// flags: the decode flags (CHK_*) -- policy_flags(0) for a bls_aggregate_* call, 0 (strict codec) for
+// partials this library encoded itself
 static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets, size_t n_pts, const uint8_t* d_pts,
-                          uint8_t* d_out, int32_t* d_status, void* ws, size_t ws_cap, hipStream_t s) {
+                          uint8_t* d_out, int32_t* d_status, void* ws, size_t ws_cap, hipStream_t s, int flags) {
   // the offsets must describe exactly the n_pts points given, in order
   if (offsets[0] != 0 || offsets[ng] != n_pts) { t_err = "offsets disagree with n_pks"; return BLS381_EARG; }
   for (size_t g = 0; g < ng; ++g)
@@ -1509,10 +1515,10 @@ static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets,
   size_t used = 0;
   int rc;
   if (is_g2) {
-    if ((rc = run_agg<fp2p_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap))) return rc;
+    if ((rc = run_agg<fp2p_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap, nullptr, flags))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(2 * ng)), dim3(KBLOCK), k_agg_compress<fp2p_t>, ng, jac, bad, d_out, d_status);
   } else {
-    if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap))) return rc;
+    if ((rc = run_agg<fp_t>(plan, ng, d_pts, ws, s, &jac, &bad, &used, ws_cap, nullptr, flags))) return rc;
     LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
   }
   return keep_until_done(c, s, hold);
@@ -1539,7 +1545,7 @@ int bls381_aggregate_pubkeys_batch_device(size_t n_groups, const uint32_t* h_off
   if (!h_offsets || !d_out48 || !d_status || !d_workspace || (n_pks && !d_pks)) return BLS381_EARG;
   hipStream_t s = (hipStream_t)stream;   // NULL = the HIP null stream (torch's default stream)
   return agg_batch_impl(c, 0, n_groups, h_offsets, n_pks, d_pks, d_out48, d_status, d_workspace,
-                        bls381_aggregate_pubkeys_batch_workspace_size(n_groups, n_pks), s);
+                        bls381_aggregate_pubkeys_batch_workspace_size(n_groups, n_pks), s, policy_flags(0));
 } catch (const std::exception& e) {
   t_err = e.what();
   return BLS381_EARG;
@@ -1562,7 +1568,7 @@ static int agg_host(int is_g2, size_t ng, const uint32_t* offsets, const uint8_t
   hipStream_t s = c->stream;
   if (npts) HIPC(hipMemcpyAsync(d_pts, pts, npts * bytes, hipMemcpyHostToDevice, s));
   if ((rc = agg_batch_impl(c, is_g2, ng, offsets, npts, d_pts, d_out, d_st, b.base + align256(b.off),
-                           b.left() > 256 ? b.left() - 256 : 0, s)))
+                           b.left() > 256 ? b.left() - 256 : 0, s, policy_flags(0))))
     return rc;
   HIPC(hipMemcpyAsync(out, d_out, ng * bytes, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(status, d_st, ng * 4, hipMemcpyDeviceToHost, s));
@@ -1887,7 +1893,8 @@ static int registry_agg_impl(Ctx* c, bls381_registry* reg, size_t ng, const uint
   const uint32_t* jac;
   const uint8_t* bad;
   size_t used = 0;
-  int rc = run_agg<fp_t>(*hold, ng, d_pks, b.base + align256(b.off), s, &jac, &bad, &used, b.left() - 256, &src);
+  int rc = run_agg<fp_t>(*hold, ng, d_pks, b.base + align256(b.off), s, &jac, &bad, &used, b.left() - 256, &src,
+                         policy_flags(0));
   if (rc) return rc;
   LAUNCH("agg_compress", s, dim3(grid_for(ng)), dim3(KBLOCK), k_agg_compress<fp_t>, ng, jac, bad, d_out, d_status);
   return keep_until_done(c, s, hold);
@@ -2506,7 +2513,7 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
       uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
       void* w1 = b.take<uint8_t>(ws1);
       if (cnt) HIPC(hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s));
-      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s))) return e;
+      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s, policy_flags(0)))) return e;
       // an invalid encoding anywhere: this partial becomes 48 zero bytes, itself invalid
       LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
       HIPC(hipStreamSynchronize(s));   // the host slice and the workspace are reused
@@ -2526,7 +2533,9 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
       const size_t wsR = agg_ws_bytes(0, 1, offR);
       int e;
       if ((e = ensure_ws(c, wsR + 4096))) return e;
-      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s);
+      // strict codec: the partials are this library's own canonical encodings, and a zero row
+      // (an error on its rank) must stay invalid -- the lax codec would decode it to (0, 2)
+      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s, 0);
     });
     if (root) {
       (void)hipStreamSynchronize(s);
@@ -2693,9 +2702,9 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
       LAUNCH("hash_cand", c->side, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
       HIPC(hipEventRecord(c->ev_join3, c->side));
     }
-    LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, chk);
+    LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
     // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-    LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, chk ? 1 : 2);
+    LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
     LAUNCH("rb_scale_g2", sb, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
            (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
     const uint32_t* sjac;

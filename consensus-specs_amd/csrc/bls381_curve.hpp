@@ -1,6 +1,6 @@
 // G1 = E(Fp): y^2 = x^3 + 4 and G2 = E'(Fp2): y^2 = x^3 + 4(1+u).
 // Jacobian coordinates, a = 0 formulas; compressed codecs following
-// specs/bls_signature.md:36-64 (strict: c_flag, x < q, infinity encodings);
+// specs/bls_signature.md:36-64 (strict) or py_ecc 1.7.0 (lax);
 // endomorphism subgroup checks; scalar multiplication.
 #pragma once
 #include "bls381_field.hpp"
@@ -192,18 +192,39 @@ BLS_NOINLINE jac_t<F> jac_mul_limbs(const aff_t<F>& a, const uint32_t* k, int nb
 // ------------------------------------------------------------- codecs -----
 enum : int { PT_OK = 0, PT_INF = 1, PT_BAD = 2 };
 
-// G1 decompress (bls_signature.md:36-52).  Returns PT_OK / PT_INF / PT_BAD.
-BLS_HD inline int g1_decompress(aff_t<fp_t>& out, const uint8_t* b48) {
+// Codecs.  Two decoders share one body, selected per call by the policy
+// (include/bls381.h BLS381_POLICY_*; DESIGN.md §3 "Codec"):
+//   strict (lax == false): specs/bls_signature.md:47-52,58-64 -- c_flag set, x < q,
+//     infinity only as the canonical 0xc0 || 00.. encoding, G2's z2 flags clear;
+//   lax (lax == true): py_ecc 1.7.0 decompress_G1 / decompress_G2 --
+//     b_flag set means infinity whatever the other bits; otherwise x = z mod 2^381
+//     (G1, G2's imaginary part) or the whole 384-bit z2 (G2's real part), reduced
+//     mod q; c_flag and x < q are never looked at.
+// Both accept every canonical encoding with the same point; the lax decoder also
+// accepts non-canonical encodings (strict PT_BAD).  g1_canonical tells them apart.
+BLS_HD inline bool g1_canonical(const uint8_t* b48) {
   const uint8_t top = b48[0];
   const int c_flag = (top >> 7) & 1, b_flag = (top >> 6) & 1, a_flag = (top >> 5) & 1;
   uint8_t tmp[48];
   for (int i = 0; i < 48; ++i) tmp[i] = b48[i];
   tmp[0] &= 0x1f;
   const fp_t x = fp_plain_from_be48(tmp);
-  if (!c_flag) return PT_BAD;
-  if (b_flag) return (a_flag == 0 && fp_is_zero(x)) ? PT_INF : PT_BAD;
-  if (!fp_plain_lt_q(x)) return PT_BAD;
-  const fp_t xm = fp_to_mont(x);
+  if (!c_flag) return false;
+  if (b_flag) return a_flag == 0 && fp_plain_is_zero(x);
+  return fp_plain_lt_q(x);
+}
+
+// G1 decompress (bls_signature.md:36-52 / py_ecc decompress_G1).  PT_OK / PT_INF / PT_BAD.
+BLS_HD inline int g1_decompress(aff_t<fp_t>& out, const uint8_t* b48, bool lax) {
+  const uint8_t top = b48[0];
+  const int b_flag = (top >> 6) & 1, a_flag = (top >> 5) & 1;
+  if (!lax && !g1_canonical(b48)) return PT_BAD;
+  if (b_flag) return PT_INF;
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b48[i];
+  tmp[0] &= 0x1f;
+  const fp_t x = fp_plain_from_be48(tmp);          // < 2^381; lax: may be >= q
+  const fp_t xm = fp_to_mont(x);                   // reduces mod q
   const fp_t rhs = fp_add(fp_mul(fp_sqr(xm), xm), G1_B_M);
   fp_t y;
   if (!fp_sqrt(y, rhs)) return PT_BAD;
@@ -233,19 +254,33 @@ BLS_INLINE int g2_y_flag(const fp2_t& y_mont) {
   return fp_plain_is_upper_half(fp_from_mont(y_mont.c0)) ? 1 : 0;
 }
 
-// G2 decompress (bls_signature.md:54-64): z1 = flags | x_im, z2 = x_re
-BLS_HD inline int g2_decompress(aff_t<fp2_t>& out, const uint8_t* b96) {
+// strict-codec acceptance of a G2 encoding (bls_signature.md:58-64)
+BLS_HD inline bool g2_canonical(const uint8_t* b96) {
   const uint8_t top = b96[0];
   const int c1 = (top >> 7) & 1, b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
-  if (b96[48] & 0xe0) return PT_BAD;      // a_flag2 == b_flag2 == c_flag2 == 0
+  if (b96[48] & 0xe0) return false;               // a_flag2 == b_flag2 == c_flag2 == 0
   uint8_t tmp[48];
   for (int i = 0; i < 48; ++i) tmp[i] = b96[i];
   tmp[0] &= 0x1f;
   const fp_t x_im = fp_plain_from_be48(tmp);
   const fp_t x_re = fp_plain_from_be48(b96 + 48);
-  if (!c1) return PT_BAD;
-  if (b1) return (a1 == 0 && fp_is_zero(x_im) && fp_is_zero(x_re)) ? PT_INF : PT_BAD;
-  if (!fp_plain_lt_q(x_im) || !fp_plain_lt_q(x_re)) return PT_BAD;
+  if (!c1) return false;
+  if (b1) return a1 == 0 && fp_plain_is_zero(x_im) && fp_plain_is_zero(x_re);
+  return fp_plain_lt_q(x_im) && fp_plain_lt_q(x_re);
+}
+
+// G2 decompress (bls_signature.md:54-64 / py_ecc decompress_G2): z1 = flags | x_im,
+// z2 = x_re (lax: all 384 bits of z2, flags included, reduced mod q)
+BLS_HD inline int g2_decompress(aff_t<fp2_t>& out, const uint8_t* b96, bool lax) {
+  const uint8_t top = b96[0];
+  const int b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
+  if (!lax && !g2_canonical(b96)) return PT_BAD;
+  if (b1) return PT_INF;
+  uint8_t tmp[48];
+  for (int i = 0; i < 48; ++i) tmp[i] = b96[i];
+  tmp[0] &= 0x1f;
+  const fp_t x_im = fp_plain_from_be48(tmp);
+  const fp_t x_re = fp_plain_from_be48(b96 + 48);
   fp2_t x;
   x.c0 = fp_to_mont(x_re);
   x.c1 = fp_to_mont(x_im);

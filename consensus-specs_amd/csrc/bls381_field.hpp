@@ -384,6 +384,14 @@ BLS_INLINE bool fp_plain_lt_q(const fp_t& a) {
   return b[13] < 0;
 }
 
+// a == 0 exactly (plain value; fp_is_zero would also accept a == q)
+BLS_INLINE bool fp_plain_is_zero(const fp_t& a) {
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 14; ++i) z |= a.w[i];
+  return z == 0;
+}
+
 // a > b
 BLS_INLINE bool fp_plain_gt(const fp_t& a, const fp_t& b) {
   int32_t d[14];

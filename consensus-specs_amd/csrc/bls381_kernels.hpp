@@ -22,7 +22,14 @@ enum : uint8_t { ST_OK = 0, ST_INF = 1, ST_BAD = 2, ST_NOSUB = 3 };
 //           and a degenerate Miller loop (miller_loop_n) yields verdict False.
 //   STRICT: every pubkey and signature must lie in G1 / G2
 //           (specs/bls_signature.md:135-136,143-144).  Aggregates never check.
-// The kernels take the policy as a `check` / `check_subgroup` flag.
+// The kernels take the policy as a flags word `check` / `check_subgroup`: bits 0-1 the
+// subgroup mode (0 none; 1 a point outside the subgroup is ST_BAD; 2 it is ST_NOSUB),
+// bit 2 (CHK_LAX) the codec -- set: py_ecc 1.7.0's lax decoder (the PYECC policy), clear:
+// the spec's strict one (bls381_curve.hpp "Codecs").
+enum : int { CHK_SUB_MASK = 3, CHK_LAX = 4 };
+// Registry entry status bit: the key decodes (lax) but is not a canonical encoding, so
+// the strict codec rejects it (k_reg_decode, agg_accumulate).
+constexpr uint8_t ST_NONCANON = 0x80;
 
 constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 // minimum waves per SIMD requested from the register allocator for the heavy
@@ -124,8 +131,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n
   uint8_t b[48];
   ld_bytes(b, pks + 48 * i, 48);
   aff_t<fp_t> a;
-  int s = g1_decompress(a, b);
-  if (s == PT_OK && check_subgroup && !g1_in_subgroup(a)) s = PT_BAD;
+  int s = g1_decompress(a, b, (check_subgroup & CHK_LAX) != 0);
+  if (s == PT_OK && (check_subgroup & CHK_SUB_MASK) && !g1_in_subgroup(a)) s = PT_BAD;
   st[i] = (uint8_t)s;
   if (s == PT_OK) soa_st_g1(out, n, i, a);
 }
@@ -138,8 +145,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2(size_t n
   const size_t i = item_index<2>();
   if (i >= n) return;
   aff_t<fp2p_t> a;
-  int s = g2_decompress(a, sigs + 96 * i);
-  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = check_subgroup == 2 ? ST_NOSUB : PT_BAD;
+  const int sub = check_subgroup & CHK_SUB_MASK;
+  int s = g2_decompress(a, sigs + 96 * i, (check_subgroup & CHK_LAX) != 0);
+  if (s == PT_OK && sub && !g2_in_subgroup(a)) s = sub == 2 ? ST_NOSUB : PT_BAD;
   if (!pr_odd()) st[i] = (uint8_t)s;
   if (s == PT_OK || s == ST_NOSUB) soa_st_g2(out, n, i, a);
 }
@@ -180,8 +188,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t
   const size_t i = item_index<1>();
   if (i >= n) return;
   aff_t<fp2_t> a;
-  int s = g2_decompress(a, sigs + 96 * i);
-  if (s == PT_OK && check_subgroup && !g2_in_subgroup(a)) s = check_subgroup == 2 ? ST_NOSUB : PT_BAD;
+  const int sub = check_subgroup & CHK_SUB_MASK;
+  int s = g2_decompress(a, sigs + 96 * i, (check_subgroup & CHK_LAX) != 0);
+  if (s == PT_OK && sub && !g2_in_subgroup(a)) s = sub == 2 ? ST_NOSUB : PT_BAD;
   st[i] = (uint8_t)s;
   if (s == PT_OK || s == ST_NOSUB) soa_st_g2_1(out, n, i, a);
 }
@@ -933,12 +942,12 @@ struct agg_chunk { uint32_t begin, end; };
 template <class F> struct pt_traits;
 template <> struct pt_traits<fp_t> {
   static constexpr int BYTES = 48;
-  __device__ static int decode(aff_t<fp_t>& a, const uint8_t* b) { return g1_decompress(a, b); }
+  __device__ static int decode(aff_t<fp_t>& a, const uint8_t* b, bool lax) { return g1_decompress(a, b, lax); }
   __device__ static bool in_subgroup(const aff_t<fp_t>& a) { return g1_in_subgroup(a); }
 };
 template <> struct pt_traits<fp2p_t> {
   static constexpr int BYTES = 96;
-  __device__ static int decode(aff_t<fp2p_t>& a, const uint8_t* b) { return g2_decompress(a, b); }
+  __device__ static int decode(aff_t<fp2p_t>& a, const uint8_t* b, bool lax) { return g2_decompress(a, b, lax); }
   __device__ static bool in_subgroup(const aff_t<fp2p_t>& a) { return g2_in_subgroup(a); }
 };
 
@@ -986,29 +995,32 @@ struct agg_reg_src {
   size_t size;            // entries in use: an entry >= size is an error (BAD), never read
 };
 
-// adds level-1 input e (compressed bytes, or a registry entry) to acc; with
-// `check` (STRICT policy, verify_multiple) a point outside the subgroup is bad
+// adds level-1 input e (compressed bytes, or a registry entry) to acc.  `check` flags
+// (CHK_*): the codec, and (STRICT policy, verify_multiple) a point outside the subgroup is bad
 template <class F, int MODE>
 __device__ __forceinline__ void agg_accumulate(jac_t<F>& acc, bool& bad, uint32_t e, const uint8_t* in_bytes,
                                                const agg_reg_src& reg, int check) {
+  const bool lax = (check & CHK_LAX) != 0;
+  const int sub = check & CHK_SUB_MASK;
   if (MODE == AGG_REGISTRY) {
     const int32_t r = reg.entry ? reg.entry[e] : -1;
     if ((r >= 0 && (size_t)r >= reg.size) || (r < 0 && !in_bytes)) { bad = true; return; }
     if (r >= 0) {
-      const uint8_t rs = reg.st[r];
+      const uint8_t rs0 = reg.st[r];
+      const uint8_t rs = (rs0 & ST_NONCANON) && !lax ? (uint8_t)ST_BAD : (uint8_t)(rs0 & ~ST_NONCANON);
       if (rs == ST_BAD) {
         bad = true;
       } else if (rs == ST_OK) {
         const aff_t<F> a = reg_ld_aff<F>(reg.aff, (size_t)r);
-        if (check && !pt_traits<F>::in_subgroup(a)) bad = true;
+        if (sub && !pt_traits<F>::in_subgroup(a)) bad = true;
         else acc = jac_add_aff(acc, a);
       }
       return;
     }
   }
   aff_t<F> a;
-  int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e);
-  if (s == PT_OK && check && !pt_traits<F>::in_subgroup(a)) s = PT_BAD;
+  int s = pt_traits<F>::decode(a, in_bytes + (size_t)pt_traits<F>::BYTES * e, lax);
+  if (s == PT_OK && sub && !pt_traits<F>::in_subgroup(a)) s = PT_BAD;
   if (s == PT_BAD) bad = true;
   else if (s == PT_OK) acc = jac_add_aff(acc, a);
 }
@@ -1139,7 +1151,9 @@ __device__ __forceinline__ bool reg_key_eq(const uint8_t* a, const uint8_t* b) {
   return d == 0;
 }
 
-// decode keys [first, first + n) in place (status + affine point)
+// decode keys [first, first + n) in place (status + affine point).  Entries serve calls
+// under either policy: a key is decoded with the lax codec, and one the strict codec
+// rejects is marked ST_NONCANON (its lax point is the only point either codec gives it).
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_reg_decode(size_t first, size_t n, size_t cap,
                                                       const uint8_t* __restrict__ keys,
                                                       uint32_t* __restrict__ aff, uint8_t* __restrict__ st) {
@@ -1147,9 +1161,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_reg_decode(size_t 
   if (t >= n) return;
   const size_t j = first + t;
   aff_t<fp_t> a;
-  const int s = g1_decompress(a, keys + 48 * j);
+  const uint8_t* k = keys + 48 * j;
+  const int s = g1_decompress(a, k, true);
   if (s == PT_OK) reg_st_g1(aff, j, a);
-  st[j] = s == PT_OK ? ST_OK : (s == PT_INF ? ST_INF : ST_BAD);
+  const uint8_t nc = s != PT_BAD && !g1_canonical(k) ? ST_NONCANON : (uint8_t)0;
+  st[j] = (uint8_t)((s == PT_OK ? ST_OK : (s == PT_INF ? ST_INF : ST_BAD)) | nc);
 }
 
 // insert entries [first, first + n) that decoded.  Equal keys share one slot,

@@ -270,20 +270,19 @@ __device__ __forceinline__ int g2_y_flag(const fp2p_t& y_mont) {
   return (int)(z1 ? up0 : up1);
 }
 
-// G2 decompress (bls_signature.md:54-64): z1 = flags | x_im (odd lane), z2 = x_re (even lane)
-__device__ inline int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96) {
+// G2 decompress (bls_signature.md:54-64 / py_ecc decompress_G2, bls381_curve.hpp):
+// z1 = flags | x_im (odd lane), z2 = x_re (even lane; lax: all 384 bits, reduced mod q)
+__device__ inline int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96, bool lax) {
   const bool odd = pr_odd();
   const uint8_t top = b96[0];
-  const int c1 = (top >> 7) & 1, b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
-  if (b96[48] & 0xe0) return PT_BAD;      // a_flag2 == b_flag2 == c_flag2 == 0
+  const int b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
+  if (!lax && !g2_canonical(b96)) return PT_BAD;
+  if (b1) return PT_INF;
   uint8_t tmp[48];
   const uint8_t* src = b96 + (odd ? 0 : 48);
   for (int i = 0; i < 48; ++i) tmp[i] = src[i];
   if (odd) tmp[0] &= 0x1f;
   const fp_t xc = fp_plain_from_be48(tmp);
-  if (!c1) return PT_BAD;
-  if (b1) return (a1 == 0 && pr_both(fp_is_zero(xc))) ? PT_INF : PT_BAD;
-  if (!pr_both(fp_plain_lt_q(xc))) return PT_BAD;
   fp2p_t x;
   x.v = fp_to_mont(xc);
   const fp2p_t rhs = fp2_add(fp2_mul(fp2_sqr(x), x), e2_k<fp2p_t>(G2_B_M));

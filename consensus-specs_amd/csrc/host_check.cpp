@@ -119,15 +119,16 @@ void hc_fp12_mul_by_line(const uint8_t* f, const uint8_t* c0, const uint8_t* c1,
 }
 void hc_final_exp(const uint8_t* a, uint8_t* o) { st12(o, final_exp(ld12(a))); }
 
-int hc_g1_decompress(const uint8_t* b48, uint8_t* aff96) {
+// lax != 0: py_ecc 1.7.0's codec, else the spec's strict one
+int hc_g1_decompress(const uint8_t* b48, uint8_t* aff96, int lax) {
   aff_t<fp_t> a;
-  const int s = g1_decompress(a, b48);
+  const int s = g1_decompress(a, b48, lax != 0);
   if (s == PT_OK) { st(aff96, a.x); st(aff96 + 48, a.y); }
   return s;
 }
-int hc_g2_decompress(const uint8_t* b96, uint8_t* aff192) {
+int hc_g2_decompress(const uint8_t* b96, uint8_t* aff192, int lax) {
   aff_t<fp2_t> a;
-  const int s = g2_decompress(a, b96);
+  const int s = g2_decompress(a, b96, lax != 0);
   if (s == PT_OK) { st2(aff192, a.x); st2(aff192 + 96, a.y); }
   return s;
 }
@@ -174,7 +175,8 @@ int hc_miller_loop(int n, const uint8_t* q192, const uint8_t* p96, uint8_t* o576
 
 // ---- whole-call semantics of the gfx950 pipelines, same headers, one thread
 // (bls381_capi.hip run_verify_batch / run_vm_batch): decode, the subgroup
-// policy (strict != 0: BLS381_POLICY_STRICT), py_ecc's infinity short circuit
+// policy (strict != 0: BLS381_POLICY_STRICT, the spec's codec and subgroup checks; else
+// py_ecc 1.7.0's lax codec and no subgroup check), py_ecc's infinity short circuit
 // (a pair with an infinite point is 1), a degenerate Miller loop -> False,
 // one final exponentiation.  Returns 1 / 0.
 static bool g1_in(const aff_t<fp_t>& a) { return g1_in_subgroup(a); }
@@ -196,8 +198,8 @@ int hc_verify(const uint8_t* pk48, const uint8_t* msg, uint32_t mlen, const uint
               int strict) {
   aff_t<fp_t> P;
   aff_t<fp2_t> S;
-  const int sp = g1_decompress(P, pk48);
-  const int ss = g2_decompress(S, sig96);
+  const int sp = g1_decompress(P, pk48, !strict);
+  const int ss = g2_decompress(S, sig96, !strict);
   if (sp == PT_BAD || ss == PT_BAD) return 0;
   if (strict && ((sp == PT_OK && !g1_in(P)) || (ss == PT_OK && !g2_in(S)))) return 0;
   aff_t<fp2_t> Q[2];
@@ -226,12 +228,12 @@ int hc_verify_multiple(size_t n, const uint8_t* pks, const uint8_t* msgs, uint32
     auto it = groups.find(key);
     if (it == groups.end()) it = groups.emplace(key, jac_infinity<fp_t>()).first;
     aff_t<fp_t> a;
-    const int s = g1_decompress(a, pks + 48 * i);
+    const int s = g1_decompress(a, pks + 48 * i, !strict);
     if (s == PT_BAD || (s == PT_OK && strict && !g1_in(a))) return 0;
     if (s == PT_OK) it->second = jac_add_aff(it->second, a);
   }
   aff_t<fp2_t> S;
-  const int ss = g2_decompress(S, sig96);
+  const int ss = g2_decompress(S, sig96, !strict);
   if (ss == PT_BAD || (ss == PT_OK && strict && !g2_in(S))) return 0;
   std::vector<aff_t<fp2_t>> Q;
   std::vector<aff_t<fp_t>> Pa;
@@ -297,11 +299,11 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   aff_t<fp_t> P;
   aff_t<fp2_t> S, H;
   g_fp_mul_count = g_fp_half_count = 0;
-  int sp = g1_decompress(P, pk48);
+  int sp = g1_decompress(P, pk48, !strict);
   if (strict && sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
   out[0] = g_fp_mul_count + g_fp_half_count / 2;
   g_fp_mul_count = g_fp_half_count = 0;
-  int ss = g2_decompress(S, sig96);
+  int ss = g2_decompress(S, sig96, !strict);
   if (strict && ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
   out[1] = g_fp_mul_count + g_fp_half_count / 2;
   g_fp_mul_count = g_fp_half_count = 0;
@@ -356,7 +358,7 @@ int hc_count_aggregate(size_t n, const uint8_t* pks, uint64_t* out) {
   jac_t<fp_t> acc = jac_infinity<fp_t>();
   for (size_t i = 0; i < n; ++i) {
     aff_t<fp_t> a;
-    const int s = g1_decompress(a, pks + 48 * i);
+    const int s = g1_decompress(a, pks + 48 * i, true);
     if (s == PT_BAD) return -1;
     if (s == PT_OK) acc = jac_add_aff(acc, a);
   }

@@ -29,8 +29,13 @@ restates py_ecc 1.7.0's published algorithms in plain Python integers:
 * Pairing: ate Miller loop over |x| in Fq12 coordinates (tower w^12 - 2w^6 + 2,
   as py_ecc) and the naive final exponentiation f^((q^12-1)/r) (Appendix A.9).
 
-Decoding strictness: the spec's checks (`bls_signature.md:47-52,58-64`: c_flag,
-x < q, infinity encodings) are enforced, as SURVEY.md A.4 prescribes.
+Decoding: two codecs.  The default is py_ecc 1.7.0's own `decompress_G1` /
+`decompress_G2`: b_flag set means infinity whatever the other bits,
+x = z mod 2^381 (G2: the imaginary part; the real part is all 384 bits of z2) reduced
+mod q by FQ / FQ2, and neither c_flag nor x < q is checked.  `strict=True` applies the
+spec's checks instead (`bls_signature.md:47-52,58-64`: c_flag, x < q, canonical
+infinity, G2's z2 flags clear) -- the codec of the strict policy.  Both give the same
+point for every canonical encoding.
 
 Domain serialisation: py_ecc 1.7.0 feeds `domain.to_bytes(8, DOMAIN_BYTEORDER)`
 into SHA-256 ("medium, recalled"); the single switch is
@@ -338,29 +343,33 @@ def compress_G1(pt) -> int:
     return x + a_flag * POW_2_381 + POW_2_383
 
 
-def decompress_G1(z: int):
-    """Strict G1 decode (bls_signature.md:47-52).  Raises ValueError."""
+def decompress_G1(z: int, strict: bool = False):
+    """py_ecc 1.7.0 `decompress_G1`; strict=True: the spec's checks
+    (bls_signature.md:47-52).  Raises ValueError."""
     if z >= 2 ** 384:
         raise ValueError("G1 encoding longer than 384 bits")
     c_flag = z >> 383
     b_flag = (z >> 382) & 1
     a_flag = (z >> 381) & 1
     x = z % POW_2_381
-    if c_flag != 1:
-        raise ValueError("c_flag must be 1")
-    if b_flag == 1:
-        if a_flag != 0 or x != 0:
+    if strict:
+        if c_flag != 1:
+            raise ValueError("c_flag must be 1")
+        if b_flag == 1 and (a_flag != 0 or x != 0):
             raise ValueError("bad infinity encoding")
+        if b_flag == 0 and x >= q:
+            raise ValueError("x >= q")
+    # py_ecc: b_flag == 1 indicates the infinity point (no other bit is looked at)
+    if b_flag == 1:
         return Z1
-    if x >= q:
-        raise ValueError("x >= q")
+    # py_ecc: FQ(x) reduces mod q; x**3 + b is taken mod q before the root
     rhs = (x * x * x + B1) % q
     y = pow(rhs, (q + 1) // 4, q)
     if (y * y) % q != rhs:
         raise ValueError("The given point is not on G1: y**2 = x**3 + b")
     if (y * 2) // q != a_flag:
         y = q - y
-    return (x, y, 1)
+    return (x % q, y, 1)
 
 
 def compress_G2(pt) -> Tuple[int, int]:
@@ -376,8 +385,10 @@ def compress_G2(pt) -> Tuple[int, int]:
     return (z1, z2)
 
 
-def decompress_G2(p: Tuple[int, int]):
-    """Strict G2 decode (bls_signature.md:58-64).  Raises ValueError."""
+def decompress_G2(p: Tuple[int, int], strict: bool = False):
+    """py_ecc 1.7.0 `decompress_G2`: x = FQ2([z2, z1 mod 2^381]), both
+    reduced mod q (z2 with its top bits); strict=True: the spec's checks
+    (bls_signature.md:58-64).  Raises ValueError."""
     z1, z2 = p
     if z1 >= 2 ** 384 or z2 >= 2 ** 384:
         raise ValueError("G2 encoding longer than 384 bits")
@@ -385,18 +396,20 @@ def decompress_G2(p: Tuple[int, int]):
     b1 = (z1 >> 382) & 1
     a1 = (z1 >> 381) & 1
     x1 = z1 % POW_2_381
-    if z2 >> 381:
-        raise ValueError("flags of z2 must be zero")
     x2 = z2
-    if c1 != 1:
-        raise ValueError("c_flag1 must be 1")
-    if b1 == 1:
-        if a1 != 0 or x1 != 0 or x2 != 0:
+    if strict:
+        if z2 >> 381:
+            raise ValueError("flags of z2 must be zero")
+        if c1 != 1:
+            raise ValueError("c_flag1 must be 1")
+        if b1 == 1 and (a1 != 0 or x1 != 0 or x2 != 0):
             raise ValueError("bad infinity encoding")
+        if b1 == 0 and (x1 >= q or x2 >= q):
+            raise ValueError("x >= q")
+    # py_ecc: b_flag1 == 1 indicates the infinity point
+    if b1 == 1:
         return Z2
-    if x1 >= q or x2 >= q:
-        raise ValueError("x >= q")
-    x = (x2, x1)
+    x = (x2 % q, x1 % q)
     y = modular_squareroot(f2_add(f2_mul(f2_sqr(x), x), B2))
     if y is None:
         raise ValueError("Failed to find a modular squareroot")
@@ -409,27 +422,35 @@ def decompress_G2(p: Tuple[int, int]):
     return pt
 
 
+def g1_canonical(pubkey) -> bool:
+    """True iff the 48-byte encoding has the strict codec's form (c_flag set, x < q,
+    infinity only as 0xc0 || 00..); decodability is not part of it."""
+    z = int.from_bytes(bytes(pubkey), "big")
+    c, b, a, x = z >> 383, (z >> 382) & 1, (z >> 381) & 1, z % POW_2_381
+    return c == 1 and ((a == 0 and x == 0) if b else x < q)
+
+
 def _to_bytes(b) -> bytes:
     return bytes(b)
 
 
-def pubkey_to_G1(pubkey) -> tuple:
+def pubkey_to_G1(pubkey, strict: bool = False) -> tuple:
     pubkey = _to_bytes(pubkey)
     if len(pubkey) != 48:
         raise ValueError("pubkey must be 48 bytes")
-    return decompress_G1(int.from_bytes(pubkey, "big"))
+    return decompress_G1(int.from_bytes(pubkey, "big"), strict)
 
 
 def G1_to_pubkey(pt) -> bytes:
     return compress_G1(pt).to_bytes(48, "big")
 
 
-def signature_to_G2(signature) -> tuple:
+def signature_to_G2(signature, strict: bool = False) -> tuple:
     signature = _to_bytes(signature)
     if len(signature) != 96:
         raise ValueError("signature must be 96 bytes")
     return decompress_G2((int.from_bytes(signature[:48], "big"),
-                          int.from_bytes(signature[48:], "big")))
+                          int.from_bytes(signature[48:], "big")), strict)
 
 
 def G2_to_signature(pt) -> bytes:
@@ -666,25 +687,26 @@ def verify_multiple(pubkeys: Sequence[bytes], message_hashes: Sequence[bytes],
         return False
 
 
-def aggregate_signatures(signatures: Sequence[bytes]) -> bytes:
+def aggregate_signatures(signatures: Sequence[bytes], strict: bool = False) -> bytes:
     o = Z2
     for s in signatures:
-        o = pt_add(_Fq2Ops, o, signature_to_G2(s))
+        o = pt_add(_Fq2Ops, o, signature_to_G2(s, strict))
     return G2_to_signature(o)
 
 
-def aggregate_pubkeys(pubkeys: Sequence[bytes]) -> bytes:
+def aggregate_pubkeys(pubkeys: Sequence[bytes], strict: bool = False) -> bytes:
     o = Z1
     for p in pubkeys:
-        o = pt_add(_FqOps, o, pubkey_to_G1(p))
+        o = pt_add(_FqOps, o, pubkey_to_G1(p, strict))
     return G1_to_pubkey(o)
 
 
 # ---------------------------------------------------------------------------
-# Spec-strict subgroup policy -- NOT py_ecc's behaviour.  bls_signature.md:135-136
-# and :143-144 ask that each pubkey be "a valid G1 point" and the signature "a
-# valid G2 point"; py_ecc 1.7.0 checks only that they decode onto the curve.
-# These give the BLS381_POLICY_STRICT column of tests/golden/bls_torsion.json.
+# Spec-strict policy -- NOT py_ecc's behaviour.  bls_signature.md:135-136 and
+# :143-144 ask that each pubkey be "a valid G1 point" and the signature "a valid
+# G2 point", in the format of :47-52,58-64; py_ecc 1.7.0 decodes laxly and checks
+# only that the points lie on the curve.  These give the BLS381_POLICY_STRICT
+# columns of tests/golden/*.json.
 # ---------------------------------------------------------------------------
 def in_G1(pt) -> bool:
     return pt_is_inf(_FqOps, pt_multiply(_FqOps, pt, r))
@@ -696,7 +718,7 @@ def in_G2(pt) -> bool:
 
 def verify_strict(message_hash: bytes, pubkey: bytes, signature: bytes, domain: int) -> bool:
     try:
-        if not in_G1(pubkey_to_G1(pubkey)) or not in_G2(signature_to_G2(signature)):
+        if not in_G1(pubkey_to_G1(pubkey, True)) or not in_G2(signature_to_G2(signature, True)):
             return False
     except (ValidationError, ValueError, AssertionError):
         return False
@@ -709,7 +731,7 @@ def verify_multiple_strict(pubkeys: Sequence[bytes], message_hashes: Sequence[by
         raise ValidationError(
             "len(pubkeys) (%s) should be equal to len(message_hashes) (%s)" % (len(pubkeys), len(message_hashes)))
     try:
-        if not all(in_G1(pubkey_to_G1(p)) for p in pubkeys) or not in_G2(signature_to_G2(signature)):
+        if not all(in_G1(pubkey_to_G1(p, True)) for p in pubkeys) or not in_G2(signature_to_G2(signature, True)):
             return False
     except (ValidationError, ValueError, AssertionError):
         return False

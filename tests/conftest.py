@@ -42,9 +42,24 @@ def native():
 
 
 @pytest.fixture(scope="session")
-def torsion():
-    """tests/golden/bls_torsion.json (make_torsion_vectors.py): points outside G1/G2,
-    with py_ecc and spec-strict verdict columns."""
+def noncanon():
+    """tests/golden/bls_noncanonical.json (make_noncanonical_vectors.py): encodings py_ecc
+    1.7.0's lax codec reads and the spec's strict codec rejects, with both columns."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "bls_noncanonical.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def torsion(noncanon):
+    """The cases on which the two policies may differ, with py_ecc and spec-strict verdict
+    columns: tests/golden/bls_torsion.json (make_torsion_vectors.py: points outside G1/G2)
+    with the verify / verify_multiple cases of bls_noncanonical.json appended, so every
+    layout test that runs the torsion cases runs the non-canonical encodings too.  The
+    aggregate lists are bls_torsion.json's (bls_noncanonical.json's have two output columns)."""
     import json
     with open(os.path.join(ROOT, "tests", "golden", "bls_torsion.json")) as f:
-        return json.load(f)
+        t = json.load(f)
+    t["verify"] = t["verify"] + noncanon["verify"]
+    t["verify_multiple"] = t["verify_multiple"] + noncanon["verify_multiple"]
+    return t

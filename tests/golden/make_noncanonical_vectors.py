@@ -1,0 +1,217 @@
+"""Generate tests/golden/bls_noncanonical.json: encodings the two codecs read differently.
+
+The reference decodes through py_ecc 1.7.0 (eth2spec/utils/bls.py:1;
+test_generators/bls/requirements.txt:1), whose `decompress_G1` / `decompress_G2`
+ are lax: b_flag = 1 means infinity whatever the other bits, x is
+z mod 2^381 (G2's real part: all of z2) reduced mod q, and neither c_flag nor
+x < q is checked.  The spec's format (specs/bls_signature.md:47-52,58-64) rejects
+all of these.  The engine's "pyecc" policy follows py_ecc, its "strict" policy the
+spec; every case here carries both columns:
+
+  verify / verify_multiple:  expected_pyecc, expected_strict (booleans)
+  aggregate_pubkeys / _sigs: output_pyecc, output_strict (hex, or null = ValueError)
+
+Consensus-relevant examples: a deposit whose pubkey or proof-of-possession has its
+c_flag cleared is valid for py_ecc (process_deposit adds the validator,
+specs/core/0_beacon-chain.md:1756-1759); `bls_aggregate_pubkeys([00 * 48])` is the
+order-3 point (0, 2), 0x80 || 00*47, under py_ecc and a ValueError under the spec.
+
+Run:  python tests/golden/make_noncanonical_vectors.py   (a few minutes on one core)
+"""
+import json
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+import bls_oracle as o  # noqa: E402
+
+q = o.q
+
+
+def enc_g1(x, a_flag, c_flag=1, b_flag=0):
+    return ((c_flag << 383) | (b_flag << 382) | (a_flag << 381) | x).to_bytes(48, "big")
+
+
+def enc_g2(x_im, x_re, a_flag, c_flag=1, b_flag=0, z2_top=0):
+    z1 = (c_flag << 383) | (b_flag << 382) | (a_flag << 381) | x_im
+    z2 = (z2_top << 381) | x_re
+    return z1.to_bytes(48, "big") + z2.to_bytes(48, "big")
+
+
+def g1_parts(pk):
+    z = int.from_bytes(pk, "big")
+    return z % 2 ** 381, (z >> 381) & 1
+
+
+def g2_parts(sig):
+    z1 = int.from_bytes(sig[:48], "big")
+    z2 = int.from_bytes(sig[48:], "big")
+    return z1 % 2 ** 381, z2, (z1 >> 381) & 1
+
+
+def agg_or_none(fn, items, strict):
+    try:
+        return fn(items, strict).hex()
+    except ValueError:
+        return None
+
+
+def g2_point_with_real_y(rng):
+    """A point of E'(Fp2) whose y has imaginary part 0 (the a_flag falls back to y_re)."""
+    while True:
+        b = rng.randrange(1, q)
+        a2 = (b * b * b - 4) * pow(3 * b, q - 2, q) % q      # Im(x^3) = 3a^2 b - b^3 = -4
+        a = pow(a2, (q + 1) // 4, q)
+        if a * a % q != a2:
+            continue
+        re = (a * a * a - 3 * a * b * b + 4) % q
+        y = pow(re, (q + 1) // 4, q)
+        if y * y % q != re:
+            continue
+        pt = ((a, b), (y, 0), o.FQ2_ONE)
+        assert o.pt_is_on_curve(o.Fq2Ops, pt, o.B2)
+        return pt
+
+
+def main():
+    rng = random.Random(0xB15_0C0D)
+    d_dep = 3                                   # DOMAIN_DEPOSIT (0_beacon-chain.md:254)
+    # a key whose x leaves room for x + q below 2^381, and one whose x does not
+    sk_lo = None
+    for k in range(2, 400):
+        x, _ = g1_parts(o.privtopub(k))
+        if x + q < 2 ** 381:
+            sk_lo = k
+            break
+    assert sk_lo is not None
+    sk = rng.randrange(1, o.r)
+    msg = bytes(rng.getrandbits(8) for _ in range(32))
+    msg2 = bytes(rng.getrandbits(8) for _ in range(32))
+    pk, pk_lo = o.privtopub(sk), o.privtopub(sk_lo)
+    sig, sig_lo = o.sign(msg, sk, d_dep), o.sign(msg, sk_lo, d_dep)
+    x_pk, a_pk = g1_parts(pk)
+    x_lo, a_lo = g1_parts(pk_lo)
+    xi, xr, a_s = g2_parts(sig)
+    xi_lo, xr_lo, a_slo = g2_parts(sig_lo)
+    inf_pk = bytes([0xC0]) + bytes(47)
+    inf_sig = bytes([0xC0]) + bytes(95)
+
+    # --- G1 encodings
+    pk_c0 = enc_g1(x_pk, a_pk, c_flag=0)                      # c_flag cleared
+    pk_lo_xq = enc_g1(x_lo + q, a_lo)                         # x + q (< 2^381)
+    pk_lo_xq_c0 = enc_g1(x_lo + q, a_lo, c_flag=0)
+    pk_zero = bytes(48)                                       # (0, 2): order 3
+    pk_x_eq_q = enc_g1(q, 0)                                  # x = q = 0 mod q: (0, 2)
+    pk_inf_junk = [enc_g1(12345, 1, b_flag=1), enc_g1(0, 0, c_flag=0, b_flag=1),
+                   bytes([0xFF]) * 48, enc_g1(q - 1, 0, b_flag=1)]
+    pk_stub = b"\x22" * 48                                    # bls.py:7 STUB_PUBKEY
+    # --- G2 encodings
+    sig_c0 = enc_g2(xi, xr, a_s, c_flag=0)
+    sig_lo_c0 = enc_g2(xi_lo, xr_lo, a_slo, c_flag=0)
+    sig_xr_q = enc_g2(xi, xr + q, a_s)                        # z2 = x_re + q (< 2^381 or not)
+    sig_xr_8q = enc_g2(xi, 0, a_s, z2_top=0)[:48] + (xr + 8 * q).to_bytes(48, "big")   # z2 flag bits set
+    sig_xi_q = enc_g2(xi + q, xr, a_s) if xi + q < 2 ** 381 else None
+    sig_z2_flags = enc_g2(xi, xr, a_s)[:48] + ((xr + 4 * q) if xr + 4 * q < 2 ** 384 else xr).to_bytes(48, "big")
+    sig_inf_junk = [enc_g2(7, 99, 1, b_flag=1), enc_g2(0, 0, 0, c_flag=0, b_flag=1),
+                    inf_sig[:95] + b"\x01", bytes([0xFF]) * 96]
+    sig_zero = bytes(96)
+    sig_stub = b"\x11" * 96                                   # bls.py:6 STUB_SIGNATURE
+    yre_pt = g2_point_with_real_y(rng)
+    sig_yre = o.G2_to_signature(yre_pt)
+
+    verify_cases = [
+        ("deposit_pk_c0", pk_c0, msg, sig),
+        ("deposit_sig_c0", pk, msg, sig_c0),
+        ("deposit_both_c0", pk_c0, msg, sig_c0),
+        ("pk_x_plus_q", pk_lo_xq, msg, sig_lo),
+        ("pk_x_plus_q_c0_sig_c0", pk_lo_xq_c0, msg, sig_lo_c0),
+        ("sig_xre_plus_q", pk, msg, sig_xr_q),
+        ("sig_xre_plus_8q_z2_flags", pk, msg, sig_xr_8q),
+        ("sig_z2_flags_reduced", pk, msg, sig_z2_flags),
+        ("pk_c0_wrong_msg", pk_c0, msg2, sig),
+        ("pk_inf_junk_sig_inf_junk", pk_inf_junk[0], msg, sig_inf_junk[0]),
+        ("pk_inf_c0_sig_inf_c0", pk_inf_junk[1], msg, sig_inf_junk[1]),
+        ("pk_ff_sig_ff", pk_inf_junk[2], msg, sig_inf_junk[3]),
+        ("pk_inf_junk_sig_inf", pk_inf_junk[3], msg, inf_sig),
+        ("pk_inf_sig_inf_junk", inf_pk, msg, sig_inf_junk[2]),
+        ("pk_inf_junk_valid_sig", pk_inf_junk[0], msg, sig),
+        ("zero_pk_sig_inf", pk_zero, msg, inf_sig),
+        ("zero_pk_sig_inf_junk", pk_zero, msg, sig_inf_junk[0]),
+        ("pk_x_eq_q_sig_inf", pk_x_eq_q, msg, inf_sig),
+        ("zero_pk_valid_sig", pk_zero, msg, sig),
+        ("valid_pk_zero_sig", pk, msg, sig_zero),
+        ("stub_pk_stub_sig", pk_stub, msg, sig_stub),
+        ("sig_y_real", pk, msg, sig_yre),
+        ("control_valid", pk, msg, sig),
+    ]
+    if sig_xi_q is not None:
+        verify_cases.append(("sig_xim_plus_q", pk, msg, sig_xi_q))
+    out = {"verify": [], "verify_multiple": [], "aggregate_pubkeys": [], "aggregate_sigs": []}
+    for kind, p, m, s in verify_cases:
+        out["verify"].append({"kind": kind, "pubkey": p.hex(), "message": m.hex(), "signature": s.hex(),
+                              "domain": str(d_dep), "expected_pyecc": o.verify(m, p, s, d_dep),
+                              "expected_strict": o.verify_strict(m, p, s, d_dep)})
+        c = out["verify"][-1]
+        print("verify", kind, c["expected_pyecc"], c["expected_strict"], flush=True)
+
+    # --- verify_multiple: attestation shapes (0_beacon-chain.md:1023-1033) with lax encodings
+    d_att = 2
+    sks = [rng.randrange(1, o.r) for _ in range(3)]
+    pks = [o.privtopub(k) for k in sks]
+    agg_sig = o.aggregate_signatures([o.sign(msg, k, d_att) for k in sks])
+    agg_pk = o.aggregate_pubkeys(pks)
+    xa, aa = g1_parts(agg_pk)
+    xs, xsr, asg = g2_parts(agg_sig)
+    agg_pk_c0 = enc_g1(xa, aa, c_flag=0)
+    agg_sig_c0 = enc_g2(xs, xsr, asg, c_flag=0)
+    pks_c0 = [enc_g1(*g1_parts(p)[:1], g1_parts(p)[1], c_flag=0) for p in pks]
+    vm_cases = [
+        ("attestation_agg_c0", [agg_pk_c0, inf_pk], [msg, msg2], agg_sig),
+        ("attestation_inf_junk", [agg_pk, pk_inf_junk[0]], [msg, msg2], agg_sig),
+        ("attestation_sig_c0", [agg_pk, inf_pk], [msg, msg2], agg_sig_c0),
+        ("members_c0_one_msg", pks_c0, [msg] * 3, agg_sig),
+        ("members_mixed_one_msg", [pks_c0[0], pks[1], pks_c0[2]], [msg] * 3, agg_sig),
+        ("member_zero_key", [pks[0], pks[1], pks[2], pk_zero], [msg] * 4, agg_sig),
+        ("empty_sig_inf_junk", [], [], sig_inf_junk[0]),
+        ("empty_sig_zero", [], [], sig_zero),
+        ("control_valid", pks, [msg] * 3, agg_sig),
+    ]
+    for kind, pl, ml, s in vm_cases:
+        out["verify_multiple"].append({
+            "kind": kind, "pubkeys": [p.hex() for p in pl], "messages": [m.hex() for m in ml],
+            "signature": s.hex(), "domain": str(d_att),
+            "expected_pyecc": o.verify_multiple(pl, ml, s, d_att),
+            "expected_strict": o.verify_multiple_strict(pl, ml, s, d_att)})
+        c = out["verify_multiple"][-1]
+        print("verify_multiple", kind, c["expected_pyecc"], c["expected_strict"], flush=True)
+
+    aggp = [("zero_key", [pk_zero]), ("zero_key_x3_is_inf", [pk_zero] * 3),
+            ("c0_and_valid", [pk_c0, pk_lo]), ("x_plus_q", [pk_lo_xq]), ("x_eq_q", [pk_x_eq_q]),
+            ("inf_junk", pk_inf_junk), ("stub", [pk_stub]), ("members_c0", pks_c0),
+            ("control", pks)]
+    for kind, pl in aggp:
+        out["aggregate_pubkeys"].append({"kind": kind, "input": [p.hex() for p in pl],
+                                         "output_pyecc": agg_or_none(o.aggregate_pubkeys, pl, False),
+                                         "output_strict": agg_or_none(o.aggregate_pubkeys, pl, True)})
+    aggs = [("c0_and_valid", [sig_c0, sig_lo]), ("xre_plus_q", [sig_xr_q]), ("xre_plus_8q", [sig_xr_8q]),
+            ("z2_flags_reduced", [sig_z2_flags]), ("inf_junk", sig_inf_junk), ("zero", [sig_zero]),
+            ("stub", [sig_stub]), ("y_real", [sig_yre]), ("y_real_neg", [o.G2_to_signature(o.pt_neg(o.Fq2Ops, yre_pt))]),
+            ("control", [sig, sig_lo])]
+    if sig_xi_q is not None:
+        aggs.append(("xim_plus_q", [sig_xi_q]))
+    for kind, sl in aggs:
+        out["aggregate_sigs"].append({"kind": kind, "input": [s.hex() for s in sl],
+                                      "output_pyecc": agg_or_none(o.aggregate_signatures, sl, False),
+                                      "output_strict": agg_or_none(o.aggregate_signatures, sl, True)})
+    # the headline py_ecc divergence of SURVEY A.4
+    assert out["aggregate_pubkeys"][0]["output_pyecc"] == "80" + "00" * 47
+    assert out["aggregate_pubkeys"][0]["output_strict"] is None
+    with open(os.path.join(HERE, "bls_noncanonical.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("bls_noncanonical.json:", {k: len(v) for k, v in out.items()})
+
+
+if __name__ == "__main__":
+    main()

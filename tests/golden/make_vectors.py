@@ -122,7 +122,8 @@ def gen_golden_batches(seed=0xB15_0001):
     for kind, pk, msg, sig, dom in items:
         out["verify"].append({"kind": kind, "pubkey": pk.hex(), "message": msg.hex(),
                               "signature": sig.hex(), "domain": str(dom),
-                              "expected": o.verify(msg, pk, sig, dom)})
+                              "expected": o.verify(msg, pk, sig, dom),
+                              "expected_strict": o.verify_strict(msg, pk, sig, dom)})
     # --- bls_verify_multiple
     vm = []
     # attestation shape: [agg(committee), inf], [m0, m1]
@@ -152,7 +153,8 @@ def gen_golden_batches(seed=0xB15_0001):
         out["verify_multiple"].append({
             "kind": kind, "pubkeys": [p.hex() for p in pkl], "messages": [m.hex() for m in ml],
             "signature": sig.hex(), "domain": str(dom),
-            "expected": o.verify_multiple(pkl, ml, sig, dom)})
+            "expected": o.verify_multiple(pkl, ml, sig, dom),
+            "expected_strict": (o.verify_multiple_strict(pkl, ml, sig, dom) if len(pkl) == len(ml) else None)})
     # --- aggregates, including cancellation to infinity and doubling
     g1 = o.privtopub(1)
     neg_g1 = o.G1_to_pubkey(o.pt_neg(o.FqOps, o.G1))
@@ -179,9 +181,9 @@ def gen_golden_batches(seed=0xB15_0001):
         out["hash_to_g2"].append({"message": msg.hex(), "domain": str(dom), "trials": trials,
                                   "affine": [hex(xr), hex(xi), hex(yr), hex(yi)],
                                   "compressed": o.G2_to_signature(h).hex()})
-    # --- encodings that must be rejected by the decoders (aggregate raises)
-    bad_g1 = [b"\x00" * 48, b"\x22" * 48, bytes([0xE0]) + b"\x00" * 47,
-              bytes([0xC0]) + b"\x00" * 46 + b"\x01", pk_x_ge_q]
+    # --- encodings both codecs reject (aggregate raises under either policy); the
+    # encodings only the strict codec rejects are in bls_noncanonical.json
+    bad_g1 = []
     # x with no square root: search deterministically
     xx = 1
     while True:
@@ -190,11 +192,24 @@ def gen_golden_batches(seed=0xB15_0001):
             break
         xx += 1
     bad_g1.append((2 ** 383 + xx).to_bytes(48, "big"))
+    bad_g1.append((xx).to_bytes(48, "big"))                 # c_flag clear as well
+    if xx + o.q < 2 ** 381:
+        bad_g1.append((2 ** 383 + xx + o.q).to_bytes(48, "big"))   # x + q: the same x mod q
     for b in bad_g1:
         out["invalid_g1"].append(b.hex())
-    bad_g2 = [b"\x00" * 96, b"\x11" * 96, bytes([0xC0]) + b"\x00" * 94 + b"\x01",
-              bytes([0x80]) + b"\x00" * 47 + bytes([0x20]) + b"\x00" * 47]
+    # G2: an x whose x^3 + 4(1 + i) has no square root in Fp2, canonical and not
+    xi = 1
+    while o.modular_squareroot(o.f2_add(o.f2_mul(o.f2_sqr((0, xi)), (0, xi)), o.B2)) is not None:
+        xi += 1
+    bad_g2 = [(2 ** 383 + xi).to_bytes(48, "big") + b"\x00" * 48,
+              (xi).to_bytes(48, "big") + (o.q).to_bytes(48, "big")]
     for b in bad_g2:
+        for strict in (False, True):
+            try:
+                o.signature_to_G2(b, strict)
+                raise AssertionError("expected undecodable")
+            except ValueError:
+                pass
         out["invalid_g2"].append(b.hex())
     return out
 

@@ -134,15 +134,82 @@ def test_golden_hash_to_g2(native, golden):
         assert [hex(xr), hex(xi), hex(yr), hex(yi)] == it["affine"]
 
 
-def test_invalid_encodings_raise_in_aggregate(native, golden):
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_invalid_encodings_raise_in_aggregate(native, golden, policy):
+    """Encodings neither codec can decode (no square root) raise under both policies."""
     from bls381_amd import bls
     _, gb = golden
-    for h in gb["invalid_g1"]:
-        with pytest.raises(ValueError):
-            bls.bls_aggregate_pubkeys([bytes.fromhex(h)])
-    for h in gb["invalid_g2"]:
-        with pytest.raises(ValueError):
-            bls.bls_aggregate_signatures([bytes.fromhex(h)])
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = policy
+    try:
+        for h in gb["invalid_g1"]:
+            with pytest.raises(ValueError):
+                bls.bls_aggregate_pubkeys([bytes.fromhex(h)])
+        for h in gb["invalid_g2"]:
+            with pytest.raises(ValueError):
+                bls.bls_aggregate_signatures([bytes.fromhex(h)])
+    finally:
+        bls.SUBGROUP_POLICY = old
+
+
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_noncanonical_aggregates_both_policies(native, noncanon, policy):
+    """bls_aggregate_pubkeys / _signatures over non-canonical encodings (bls_noncanonical.json):
+    py_ecc 1.7.0's bytes under "pyecc" (e.g. [00 * 48] -> 0x80 || 00*47, the order-3 point),
+    ValueError where the spec's codec rejects an input under "strict" -- through the shim,
+    the batch entry point (one group per case), the registry and the SURVEY names."""
+    import ctypes
+    from bls381_amd import bls
+    from bls381_amd.registry import PubkeyRegistry
+    col = "output_" + policy
+    h = bytes.fromhex
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = policy
+    native.set_subgroup_policy(policy)
+    reg = PubkeyRegistry(256)
+    try:
+        for c in noncanon["aggregate_pubkeys"]:
+            keys = [h(p) for p in c["input"]]
+            if c[col] is None:
+                with pytest.raises(ValueError):
+                    bls.bls_aggregate_pubkeys(keys)
+            else:
+                assert bls.bls_aggregate_pubkeys(keys).hex() == c[col], (c["kind"], policy)
+        for c in noncanon["aggregate_sigs"]:
+            sigs = [h(s) for s in c["input"]]
+            if c[col] is None:
+                with pytest.raises(ValueError):
+                    bls.bls_aggregate_signatures(sigs)
+            else:
+                assert bls.bls_aggregate_signatures(sigs).hex() == c[col], (c["kind"], policy)
+        # one batch, one group per case
+        groups = [[h(p) for p in c["input"]] for c in noncanon["aggregate_pubkeys"]]
+        off = np.cumsum([0] + [len(g) for g in groups]).astype(np.uint32)
+        outs, st = native.aggregate_pubkeys_batch(off, b"".join(b"".join(g) for g in groups))
+        for c, o, s in zip(noncanon["aggregate_pubkeys"], outs, st):
+            assert (o.hex() if s == 0 else None) == c[col], (c["kind"], policy)
+        # the registry decodes laxly once and serves both policies (ST_NONCANON entries)
+        ent = reg.add([k for g in groups for k in g])
+        for i, c in enumerate(noncanon["aggregate_pubkeys"]):
+            members = [int(ent[j]) for j in range(off[i], off[i + 1])]
+            if any(m < 0 for m in members):          # a key neither codec decodes is never an entry
+                assert c["output_pyecc"] is None
+                continue
+            if c[col] is None:
+                with pytest.raises(ValueError):
+                    reg.aggregate_indices([members])
+            else:
+                assert reg.aggregate_indices([members])[0].hex() == c[col], (c["kind"], policy)
+        L = native.lib()
+        for c in noncanon["aggregate_sigs"]:
+            sigs = b"".join(h(s) for s in c["input"])
+            out = ctypes.create_string_buffer(96)
+            rc = L.bls381_aggregate_g2(len(c["input"]), sigs, out)
+            assert (out.raw.hex() if rc == 0 else None) == c[col], (c["kind"], policy)
+    finally:
+        reg.close()
+        bls.SUBGROUP_POLICY = old
+        native.set_subgroup_policy("pyecc")
 
 
 # ----------------------------------------------------- edge cases (§4, A.5-7)
@@ -209,7 +276,8 @@ def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
     launches of several rounds of waves with a ragged last wave).  The tiled verdicts equal the
     untiled batch's, which equal the fixtures' column for the policy."""
     _, gb = golden
-    cases = [(c, c["expected"]) for c in gb["verify"] if len(bytes.fromhex(c["message"])) == 32]
+    gcol = "expected" if policy == "pyecc" else "expected_strict"
+    cases = [(c, c[gcol]) for c in gb["verify"] if len(bytes.fromhex(c["message"])) == 32]
     cases += [(c, c["expected_" + policy]) for c in torsion["verify"]]
     assert all(len(bytes.fromhex(c["message"])) == 32 for c, _ in cases)
 
@@ -828,8 +896,9 @@ def test_verify_multiple_grouped_device(native, golden, torsion, policy):
     stream = torch.cuda.current_stream(dev)
     h = bytes.fromhex
     _, gb = golden
+    gcol = "expected" if policy == "pyecc" else "expected_strict"
     cases = [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
-              c["expected"]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
+              c[gcol]) for c in gb["verify_multiple"] if len(c["pubkeys"]) == len(c["messages"])]
     cases += [([h(p) for p in c["pubkeys"]], [h(m) for m in c["messages"]], h(c["signature"]), int(c["domain"]),
                c["expected_" + policy]) for c in torsion["verify_multiple"]]
     rng = random.Random(0xB15_0C0D)
@@ -896,7 +965,7 @@ def test_verify_multiple_grouped_device(native, golden, torsion, policy):
 
 
 # ------------------------------------ native multi-GPU ABI over RCCL
-def _comm_checks(native, golden, torsion):
+def _comm_checks(native, golden, torsion, noncanon):
     from bls381_amd import comm
     _, gb = golden
     h = bytes.fromhex
@@ -909,6 +978,12 @@ def _comm_checks(native, golden, torsion):
         assert got == want, c["kind"]
     for c in gb["aggregate_pubkeys"] + torsion["aggregate_pubkeys"]:
         assert comm.aggregate_pubkeys([h(p) for p in c["input"]]).hex() == c["output"], c["kind"]
+    for c in noncanon["aggregate_pubkeys"]:       # py_ecc's lax codec on every rank's slice
+        if c["output_pyecc"] is None:
+            with pytest.raises(ValueError):
+                comm.aggregate_pubkeys([h(p) for p in c["input"]])
+        else:
+            assert comm.aggregate_pubkeys([h(p) for p in c["input"]]).hex() == c["output_pyecc"], c["kind"]
     keys = [O.privtopub(k) for k in range(1, 41)]
     assert comm.aggregate_pubkeys([keys[i % 40] for i in range(1000)]) == O.privtopub(
         sum((i % 40) + 1 for i in range(1000)))
@@ -922,7 +997,7 @@ def _comm_checks(native, golden, torsion):
     assert comm.verify_multiple_batch(off, pks, msgs, 32, sigs, doms) == [w for _, w in vms * 2]
 
 
-def test_native_comm_rccl_world1(native, golden, torsion):
+def test_native_comm_rccl_world1(native, golden, torsion, noncanon):
     """The library's own RCCL communicator (ncclCommInitRank through dlopen), one rank: the
     collective entry points give the single-GPU verdicts and bytes.  Multi-rank RCCL on a
     one-GPU box is refused by RCCL itself (duplicate GPU), see the virtual-rank test."""
@@ -930,21 +1005,21 @@ def test_native_comm_rccl_world1(native, golden, torsion):
     comm.init(1, 0, comm.unique_id())
     try:
         assert comm.size() == 1 and comm.rank() == 0
-        _comm_checks(native, golden, torsion)
+        _comm_checks(native, golden, torsion, noncanon)
     finally:
         comm.destroy()
     assert comm.size() == 0
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])
-def test_native_comm_virtual_ranks(native, golden, torsion, world):
+def test_native_comm_virtual_ranks(native, golden, torsion, noncanon, world):
     """N ranks on one GPU (bls381_comm_init_virtual): per-rank partials by distinct message,
     rank-0 product + single final exponentiation, contiguous aggregation ranges -- no PyTorch."""
     from bls381_amd import comm
     comm.init_virtual(world)
     try:
         assert comm.size() == world
-        _comm_checks(native, golden, torsion)
+        _comm_checks(native, golden, torsion, noncanon)
     finally:
         comm.destroy()
 
@@ -957,11 +1032,9 @@ def test_randomized_batch_matches_per_item_verdicts(native, golden, torsion, pol
     the default per-item pipeline (py_ecc's, or the strict column)."""
     import os as _os
     _, gb = golden
-    items = [(c, c["expected"]) for c in gb["verify"]]
+    gcol = "expected" if policy == "pyecc" else "expected_strict"
+    items = [(c, c[gcol]) for c in gb["verify"]]
     items += [(c, c["expected_" + policy]) for c in torsion["verify"]]
-    if policy == "strict":
-        items = [(c, e) for c, e in items if "expected_strict" in c] + [(c, e) for c, e in items
-                                                                        if "expected_strict" not in c]
     pks = b"".join(bytes.fromhex(c["pubkey"]) for c, _ in items)
     msgs = b"".join(bytes.fromhex(c["message"]) for c, _ in items)
     sigs = b"".join(bytes.fromhex(c["signature"]) for c, _ in items)
@@ -969,8 +1042,7 @@ def test_randomized_batch_matches_per_item_verdicts(native, golden, torsion, pol
     native.set_subgroup_policy(policy)
     try:
         want = list(native.verify_batch(pks, msgs, sigs, doms))
-        if policy == "pyecc":
-            assert want == [e for _, e in items]
+        assert want == [e for _, e in items]
         for B in (2, 8, 64):
             got = native.verify_batch_randomized(pks, msgs, sigs, doms, _os.urandom(32), B)
             assert list(got) == want, B

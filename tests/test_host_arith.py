@@ -234,7 +234,7 @@ def test_codecs_and_subgroups(L, golden):
     buf = ctypes.create_string_buffer(192)
     for c in vec["priv_to_pub"]:
         pk = bytes.fromhex(c["output"][2:])
-        assert L.hc_g1_decompress(pk, buf) == 0
+        assert L.hc_g1_decompress(pk, buf, 1) == 0
         assert O.pubkey_to_G1(pk) == (i48(buf.raw[:48]), i48(buf.raw[48:96]), 1)
         out = ctypes.create_string_buffer(48)
         L.hc_g1_compress_aff(buf.raw[:96], out)
@@ -242,19 +242,23 @@ def test_codecs_and_subgroups(L, golden):
         assert L.hc_g1_in_subgroup(buf.raw[:96]) == 1
     for c in vec["sign_msg"][::5]:
         sig = bytes.fromhex(c["output"][2:])
-        assert L.hc_g2_decompress(sig, buf) == 0
+        assert L.hc_g2_decompress(sig, buf, 1) == 0
         a = O.signature_to_G2(sig)
         assert (i96(buf.raw[:96]), i96(buf.raw[96:192])) == (a[0], a[1])
         out = ctypes.create_string_buffer(96)
         L.hc_g2_compress_aff(buf.raw, out)
         assert out.raw == sig
         assert L.hc_g2_in_subgroup(buf.raw) == 1
-    for h in gb["invalid_g1"]:
-        assert L.hc_g1_decompress(bytes.fromhex(h), buf) == 2
-    for h in gb["invalid_g2"]:
-        assert L.hc_g2_decompress(bytes.fromhex(h), buf) == 2
-    assert L.hc_g1_decompress(bytes([0xC0]) + b"\x00" * 47, buf) == 1
-    assert L.hc_g2_decompress(bytes([0xC0]) + b"\x00" * 95, buf) == 1
+    for lax in (0, 1):
+        for h in gb["invalid_g1"]:
+            assert L.hc_g1_decompress(bytes.fromhex(h), buf, lax) == 2
+        for h in gb["invalid_g2"]:
+            assert L.hc_g2_decompress(bytes.fromhex(h), buf, lax) == 2
+        assert L.hc_g1_decompress(bytes([0xC0]) + b"\x00" * 47, buf, lax) == 1
+        assert L.hc_g2_decompress(bytes([0xC0]) + b"\x00" * 95, buf, lax) == 1
+    # b_flag with x = q: the strict codec's infinity needs x == 0 exactly (not x == 0 mod q)
+    xq = bytearray(O.q.to_bytes(48, "big")); xq[0] |= 0xC0
+    assert L.hc_g1_decompress(bytes(xq), buf, 0) == 2 and L.hc_g1_decompress(bytes(xq), buf, 1) == 1
     s = M.sqrt_fp((5 ** 3 + 4) % q)
     assert L.hc_g1_in_subgroup(b48(5) + b48(s)) == 0
     x, y = M.map_candidate(b"\x11" * 32, b"\x00" * 8)

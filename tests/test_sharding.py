@@ -181,8 +181,9 @@ def test_sharded_aggregate_pubkeys_gloo_world2():
     res = _run(keys, kind="agg")
     want = O.privtopub(sum(range(1, 8)))
     assert res == {0: want, 1: want}
-    # an invalid encoding on rank 1's half raises on both ranks
-    res = _run(keys[:6] + [b"\x01" * 48], kind="agg")
+    # an encoding neither codec decodes (x^3 + 4 not a square) on rank 1's half raises on both ranks
+    x = next(x for x in range(1, 100) if pow((x ** 3 + 4) % O.q, (O.q - 1) // 2, O.q) != 1)
+    res = _run(keys[:6] + [(2 ** 383 + x).to_bytes(48, "big")], kind="agg")
     assert res == {0: "ValueError", 1: "ValueError"}
     # fewer keys than ranks: the empty shard contributes infinity
     res = _run(keys[:1], kind="agg")

@@ -82,14 +82,72 @@ def test_host_pipeline_torsion_verdicts(L, torsion, strict):
 
 @pytest.mark.parametrize("strict", [0, 1])
 def test_host_pipeline_golden_verdicts(L, golden, strict):
-    """The ordinary golden batches have the same verdicts under either policy."""
+    """The golden batches' verdict column of each policy (they differ only on the
+    non-canonical encodings the batches hold: the zero key, x = q, the stub encodings)."""
     _, gb = golden
+    col = "expected_strict" if strict else "expected"
     for c in gb["verify"]:
-        assert _host_verify(L, c, strict) == int(c["expected"]), c["kind"]
+        assert _host_verify(L, c, strict) == int(c[col]), c["kind"]
     for c in gb["verify_multiple"]:
         if len(c["pubkeys"]) != len(c["messages"]):
             continue
-        assert _host_verify_multiple(L, c, strict) == int(c["expected"]), c["kind"]
+        assert _host_verify_multiple(L, c, strict) == int(c[col]), c["kind"]
+
+
+def test_noncanonical_fixtures_match_oracle(noncanon):
+    """bls_noncanonical.json recomputed by the oracle: py_ecc's lax codec
+    and the spec's strict one (bls_signature.md:47-52,58-64), verdicts and aggregate bytes."""
+    for c in noncanon["verify"][::2]:
+        a = (_h(c["message"]), _h(c["pubkey"]), _h(c["signature"]), int(c["domain"]))
+        assert O.verify(*a) == c["expected_pyecc"], c["kind"]
+        assert O.verify_strict(*a) == c["expected_strict"], c["kind"]
+    for name, fn in (("aggregate_pubkeys", O.aggregate_pubkeys), ("aggregate_sigs", O.aggregate_signatures)):
+        for c in noncanon[name]:
+            for strict, col in ((False, "output_pyecc"), (True, "output_strict")):
+                try:
+                    got = fn([_h(x) for x in c["input"]], strict).hex()
+                except ValueError:
+                    got = None
+                assert got == c[col], (name, c["kind"], col)
+    kinds = {c["kind"]: c for c in noncanon["aggregate_pubkeys"]}
+    assert kinds["zero_key"]["output_pyecc"] == "80" + "00" * 47 and kinds["zero_key"]["output_strict"] is None
+    v = {c["kind"]: c for c in noncanon["verify"]}
+    assert v["deposit_pk_c0"]["expected_pyecc"] and not v["deposit_pk_c0"]["expected_strict"]
+
+
+def test_host_codecs_noncanonical(L, noncanon):
+    """The device headers' two decoders (host build) on every non-canonical encoding:
+    the lax one gives py_ecc's point (oracle), the strict one rejects what the spec rejects."""
+    buf = ctypes.create_string_buffer(192)
+    i48 = lambda b: int.from_bytes(b, "big")
+    pks = {p for c in noncanon["verify"] for p in [c["pubkey"]]}
+    pks |= {p for c in noncanon["aggregate_pubkeys"] for p in c["input"]}
+    for hx in sorted(pks):
+        b = _h(hx)
+        for strict in (False, True):
+            try:
+                want = O.pubkey_to_G1(b, strict)
+                ws = 1 if want[2] == 0 else 0
+            except ValueError:
+                want, ws = None, 2
+            s = L.hc_g1_decompress(b, buf, 0 if strict else 1)
+            assert s == ws, (hx, strict)
+            if s == 0:
+                assert (i48(buf.raw[:48]), i48(buf.raw[48:96])) == (want[0], want[1]), hx
+    sigs = {c["signature"] for c in noncanon["verify"]} | {s for c in noncanon["aggregate_sigs"] for s in c["input"]}
+    for hx in sorted(sigs):
+        b = _h(hx)
+        for strict in (False, True):
+            try:
+                want = O.signature_to_G2(b, strict)
+                ws = 1 if want[2] == O.FQ2_ZERO else 0
+            except ValueError:
+                want, ws = None, 2
+            s = L.hc_g2_decompress(b, buf, 0 if strict else 1)
+            assert s == ws, (hx, strict)
+            if s == 0:
+                got = ((i48(buf.raw[:48]), i48(buf.raw[48:96])), (i48(buf.raw[96:144]), i48(buf.raw[144:192])))
+                assert got == (want[0], want[1]), hx
 
 
 _ASAN_RUNNER = r"""
@@ -99,7 +157,8 @@ with open(sys.argv[2]) as f: gb = json.load(f)
 with open(sys.argv[3]) as f: tor = json.load(f)
 h = bytes.fromhex
 bad = 0
-for src, col in ((gb, "expected"), (tor, "expected_pyecc")):
+nc = json.load(open(sys.argv[4]))
+for src, col in ((gb, "expected"), (tor, "expected_pyecc"), (nc, "expected_pyecc")):
     for c in src["verify"]:
         m = h(c["message"])
         v = L.hc_verify(h(c["pubkey"]), m, len(m), h(c["signature"]), int(c["domain"]).to_bytes(8, "big"), 0)
@@ -133,7 +192,8 @@ def test_sanitized_host_build_over_golden_batches(tmp_path):
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     g = os.path.join(ROOT, "tests", "golden")
     res = subprocess.run([sys.executable, str(runner), lib, os.path.join(g, "bls_golden_batches.json"),
-                          os.path.join(g, "bls_torsion.json")], env=env, capture_output=True, text=True,
+                          os.path.join(g, "bls_torsion.json"), os.path.join(g, "bls_noncanonical.json")],
+                         env=env, capture_output=True, text=True,
                          timeout=600)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     assert "ERROR: AddressSanitizer" not in res.stderr and "runtime error" not in res.stderr, res.stderr[-4000:]
@@ -149,5 +209,6 @@ def test_line_pair_knob_host_build_over_golden_batches(tmp_path):
     runner.write_text(_ASAN_RUNNER)
     g = os.path.join(ROOT, "tests", "golden")
     res = subprocess.run([sys.executable, str(runner), lib, os.path.join(g, "bls_golden_batches.json"),
-                          os.path.join(g, "bls_torsion.json")], capture_output=True, text=True, timeout=600)
+                          os.path.join(g, "bls_torsion.json"), os.path.join(g, "bls_noncanonical.json")],
+                         capture_output=True, text=True, timeout=600)
     assert res.returncode == 0 and "mismatches 0" in res.stdout, res.stdout[-2000:] + res.stderr[-2000:]
