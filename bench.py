@@ -8,9 +8,15 @@ One step = one `bls381_verify_batch_device` over the whole batch (decode G1 +
 subgroup, decode G2 + subgroup, hash_to_G2, 2-pair Miller loop, final
 exponentiation, verdict), inputs resident in HBM.
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N`): every rank verifies its
-own 2^16 batch (independent items shard with no data-path collective; weak
-scaling); barrier + synchronize around the timed steps, max over ranks.
+Multi-GPU: every rank verifies its own 2^16 batch (independent items shard with
+no data-path collective; weak scaling); barrier + synchronize around the timed
+steps, max over ranks.  Launched either by `torch.distributed.run --nproc-per-node
+N ... bench.py --gpus N` (WORLD_SIZE set: this process is one rank) or as plain
+`bench.py --gpus N` with WORLD_SIZE unset: the process then only launches N child
+ranks (subprocesses with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set; it never
+touches the GPU itself) and relays rank 0's JSON line.  Either way a world that is
+not N ranks is an error, and the line carries `rccl_world` and every rank's
+ms_per_step.
 
 Also reported (secondary lines in the same JSON object):
 - "aggregation": committee pubkey aggregation alone (1024 committees x 128);
@@ -70,7 +76,65 @@ def parse():
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
                     help="subgroup policy of the headline line (bls.SUBGROUP_POLICY)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: the ranks join a gloo world, report it and exit")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without WORLD_SIZE: start N rank processes and relay rank 0's line.
+    This process never initialises the GPU (device_count() does not, on this image), and the
+    ranks are children, not an exec of this process."""
+    import subprocess
+    n = args.gpus
+    if not args.dry_run:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            sys.stderr.write("bench.py --gpus %d: only %d device(s) visible\n" % (n, have))
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0].decode()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if lines:
+        print(lines[-1], flush=True)
+    bad = [rc for rc in rcs if rc != 0]
+    if bad or not lines:
+        sys.stderr.write("bench.py --gpus %d: rank exit codes %s\n" % (n, rcs))
+        return bad[0] if bad else 1
+    return 0
+
+
+def dry_run(args, world, rank):
+    """The rank side of the launcher check: a gloo world on the CPU, no device touched."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = dist.get_world_size()
+        ranks = [None] * got
+        dist.all_gather_object(ranks, rank)
+        dist.destroy_process_group()
+    else:
+        got, ranks = 1, [0]
+    if got != args.gpus:
+        raise SystemExit("world is %d ranks, --gpus %d" % (got, args.gpus))
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "rccl_world": got, "ranks": ranks}))
 
 
 def make_workload(native, n, seed):
@@ -749,14 +813,23 @@ def bench_latency(native, pks, msgs, sigs, expected):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+    if args.dry_run:
+        dry_run(args, world, rank)
+        return
     import torch
     import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("RCCL world is %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
     torch.cuda.set_device(local_rank)
     from bls381_amd import _native as native
     native.init(local_rank)
@@ -798,10 +871,13 @@ def main():
     got = d_ver.cpu().numpy().astype(bool)
     if not np.array_equal(got, expected):
         raise SystemExit("verdict mismatch on rank %d: %d wrong" % (rank, int((got != expected).sum())))
+    rank_ms = [1e3 * elapsed / args.steps]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rank_ms = [1e3 * float(x.item()) / args.steps for x in allt]
+        elapsed = max(float(x.item()) for x in allt)
     total_items = n * args.steps * world
     value = total_items / elapsed
 
@@ -850,12 +926,18 @@ def main():
         if world > 1:
             dist.barrier()
         a_steps = max(args.steps, 3)
-        native.profile_enable(True)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a_steps):
             astep()
         torch.cuda.synchronize()
         at = time.perf_counter() - t0
+        # per-kernel HIP-event times for the roofline from extra, untimed steps (the
+        # headline rate carries no profiling events)
+        native.profile_enable(True)
+        for _ in range(2):
+            astep()
+        torch.cuda.synchronize()
         aprof = native.profile_read()
         native.profile_enable(False)
         if world > 1:
@@ -940,6 +1022,8 @@ def main():
         "value": round(value, 2),
         "unit": "verifications/s",
         "n_gpus": world,
+        "rccl_world": dist.get_world_size() if world > 1 else 1,
+        "rank_ms_per_step": [round(x, 3) for x in rank_ms],
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),

@@ -39,8 +39,12 @@ def build_hip(force=False, extra=()):
     deps = [os.path.join(CSRC, f) for f in HIP_SOURCES + HEADERS] + [os.path.join(INC, "bls381.h")]
     if not force and _newer(out, deps):
         return out
+    # built beside the target and renamed into place, so a snapshot of the tree taken while
+    # hipcc runs (a GPU call) sees the old library or the new one, never a partial file
+    tmp = out + ".partial"
     _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INC, "-I", CSRC,
-          *extra, *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", out])
+          *extra, *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", tmp])
+    os.replace(tmp, out)
     return out
 
 

@@ -270,15 +270,17 @@ size_t verify_nf(size_t n) { return n <= BLS_ML_OCT_MAX_N ? 2 * n : n; }
 #endif
 bool verify_split(size_t n);
 size_t verify_split_chunk(size_t n) { return verify_split(n) ? std::min<size_t>(n, BLS_ML_SPLIT_CHUNK) : 0; }
-size_t verify_ws_size(size_t n) {
-  const size_t ch = verify_split_chunk(n);
+// lines = false: a workspace for the decodes and the hash only (no split-loop line buffer;
+// the randomized path's own decode/hash workspace, whose pairings run elsewhere)
+size_t verify_ws_size(size_t n, bool lines = true) {
+  const size_t ch = lines ? verify_split_chunk(n) : 0;
   return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
          align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) + 1024;
 }
-VerifyWs carve_verify(void* ws, size_t n) {
+VerifyWs carve_verify(void* ws, size_t n, bool lines = true) {
   Bump b(ws);
   VerifyWs w;
-  const size_t ch = verify_split_chunk(n);
+  const size_t ch = lines ? verify_split_chunk(n) : 0;
   w.ml_L = ch ? b.take<uint32_t>(ML_L_WORDS_PER_ITEM * ch) : nullptr;
   w.ml_st = ch ? b.take<uint8_t>(ch) : nullptr;
   w.pk_aff = b.take<uint32_t>(2 * FP_LIMBS * n);
@@ -383,6 +385,9 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
   HIPC(hipEventRecord(c->ev_join, c->side));
 #else
+  // order 2 skipped decode_g1 above (it runs after decode_g2 on the side stream when that
+  // is built in); here decode_g2 is on the main stream, so decode_g1 goes first on the side
+  if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
   HIPC(hipEventRecord(c->ev_join, c->side));
   LAUNCH("decode_g2", s, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
 #endif
@@ -2217,6 +2222,19 @@ int nccl_fail(RcclApi* api, const char* what, ncclResult_t r) {
     if (r__ != ncclSuccess) return nccl_fail(api, #x, r__);      \
   } while (0)
 
+// Record-and-continue forms for the collective phases: a rank that fails still issues every
+// collective its peers will (else they block in RCCL forever); the first error is kept in `err`.
+#define HIPC_KEEP(err, x)                                            \
+  do {                                                               \
+    hipError_t e__ = (x);                                            \
+    if (e__ != hipSuccess && !(err)) (err) = fail(#x, e__);          \
+  } while (0)
+#define NCCLC_KEEP(err, api, x)                                      \
+  do {                                                               \
+    ncclResult_t r__ = (x);                                          \
+    if (r__ != ncclSuccess && !(err)) (err) = nccl_fail(api, #x, r__); \
+  } while (0)
+
 // Fp12 value (SoA, one item) -> 576 canonical bytes, or 576 zero bytes when its
 // status is not OK (an honest partial product is never 0; a zero row makes the
 // gathered product 0 and the verdict False on rank 0)
@@ -2437,13 +2455,14 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
   if (local) {
     (void)hipStreamSynchronize(s);
     if (cm->virt) return local;
-    if (hipMemset(d_rows + 576 * R, 0, 576) != hipSuccess) return local;   // row unusable: RCCL cannot help
+    // a zero row (never an honest partial), ordered before the all-gather on the same stream
+    if (hipMemsetAsync(d_rows + 576 * R, 0, 576, s) != hipSuccess) return local;   // row unusable: RCCL cannot help
   }
   if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 576 * R, d_rows, 576, ncclUint8, cm->comm, s));
   if (is_root(cm)) {   // one final exponentiation, on rank 0 (verdict 0 if it cannot run)
-    HIPC(hipMemsetAsync(d_v, 0, 1, s));
     const int root = local_stage([&]() -> int {
       int lrc;
+      HIPC(hipMemsetAsync(d_v, 0, 1, s));
       if ((lrc = ensure_ws(c, 12 * FPW * R * 4 + 4 * R + 65536))) return lrc;
       Bump b(c->ws, c->ws_cap);
       uint32_t* g = b.take<uint32_t>(12 * FP_LIMBS * R);
@@ -2468,7 +2487,7 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
     });
     if (root) {
       (void)hipStreamSynchronize(s);
-      (void)hipMemset(d_v, 0, 1);
+      (void)hipMemsetAsync(d_v, 0, 1, s);
       if (!local) local = root;
     }
   }
@@ -2521,7 +2540,7 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
     });
     if (lrc) {
       (void)hipStreamSynchronize(s);
-      (void)hipMemset(part, 0, 48);   // 48 zero bytes: not an encoding, the sum is flagged
+      (void)hipMemsetAsync(part, 0, 48, s);   // 48 zero bytes: not an encoding, the sum is flagged
       if (!local) local = lrc;
     }
   }
@@ -2539,9 +2558,9 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
     });
     if (root) {
       (void)hipStreamSynchronize(s);
-      const int32_t err = BLS381_EHIP;
-      (void)hipMemset(d_sum, 0, 48);
-      (void)hipMemcpy(d_st + 1, &err, 4, hipMemcpyHostToDevice);
+      static const int32_t err = BLS381_EHIP;   // a copy source that outlives the queued copy
+      (void)hipMemsetAsync(d_sum, 0, 48, s);
+      (void)hipMemcpyAsync(d_st + 1, &err, 4, hipMemcpyHostToDevice, s);
       if (!local) local = root;
     }
   }
@@ -2597,14 +2616,19 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
     uint8_t* d_rows;
     const size_t piece = std::min(width, COMM_ROWS_BYTES / (R + 1));
     if ((rc = comm_rows(cm, piece * (R + 1), &d_rows))) return rc;   // fits by construction
-    for (size_t at = 0; at < width; at += piece) {   // same piece count on every rank (width is)
+    // every rank issues the same all-gathers (width and piece are the same everywhere) even after
+    // an error of its own, so no peer waits on a collective this rank skipped
+    int err = 0;
+    for (size_t at = 0; at < width; at += piece) {
       const size_t w = std::min(piece, width - at);
-      HIPC(hipMemcpyAsync(d_rows + piece * R, rows.data() + width * (size_t)cm->rank + at, w, hipMemcpyHostToDevice, s));
-      NCCLC(api, api->all_gather(d_rows + piece * R, d_rows, w, ncclUint8, cm->comm, s));
+      HIPC_KEEP(err, hipMemcpyAsync(d_rows + piece * R, rows.data() + width * (size_t)cm->rank + at, w,
+                                    hipMemcpyHostToDevice, s));
+      NCCLC_KEEP(err, api, api->all_gather(d_rows + piece * R, d_rows, w, ncclUint8, cm->comm, s));
       for (size_t q = 0; q < R; ++q)
-        HIPC(hipMemcpyAsync(rows.data() + width * q + at, d_rows + w * q, w, hipMemcpyDeviceToHost, s));
-      HIPC(hipStreamSynchronize(s));
+        HIPC_KEEP(err, hipMemcpyAsync(rows.data() + width * q + at, d_rows + w * q, w, hipMemcpyDeviceToHost, s));
+      HIPC_KEEP(err, hipStreamSynchronize(s));
     }
+    if (err) return err;
   }
   for (size_t q = 0; q < R; ++q) {
     const size_t qlo = q * base + (q < extra ? q : extra), qcnt = base + (q < extra ? 1 : 0);
@@ -2630,7 +2654,7 @@ size_t rb_slots(size_t n, size_t B) { return ((n + B - 1) / B) * (B / 2 + 1); }
 size_t rb_ml_chunk(size_t n, size_t B) { return std::min<size_t>(((n + B - 1) / B) * (B / 2), RB_ML_CHUNK); }
 size_t rb_ws_size(size_t n, size_t B) {
   const size_t nb = (n + B - 1) / B, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
-  size_t s = verify_ws_size(n) + 4 * 65536;
+  size_t s = verify_ws_size(n, false) + 4 * 65536;   // decodes + hash: no split-loop line buffer
   s += align256(2 * FPW * n) + 3 * align256(n) + align256(6 * FPW * n) + align256(n);   // R1, statuses, R2, zeros
   const size_t ch = nb + n / CHUNK_L1 + 1;                                              // R2 sums per sub-batch
   s += 3 * (align256(ch * sizeof(agg_chunk)) + align256(ch * 6 * FPW) + align256(ch));
@@ -2649,7 +2673,7 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
                           size_t ws_cap, hipStream_t s, uint64_t* stats) {
   const size_t nb = (n + B - 1) / B, hb = B / 2, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
   Bump b(ws, ws_cap);
-  VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n)), n);
+  VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n, false)), n, false);
   uint32_t* r1 = b.take<uint32_t>(2 * FP_LIMBS * n);
   uint8_t* r1_st = b.take<uint8_t>(n);
   uint8_t* cls = b.take<uint8_t>(n);

@@ -133,49 +133,57 @@ template <typename K>
 static double time_kernel(K kern, uint64_t* d, int blocks, int reps) {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, 1u);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, 1u);   // warm-up launch
   CHECK(hipDeviceSynchronize());
   CHECK(hipEventRecord(e0));
   for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, 0, d, (uint32_t)r);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms = 0; CHECK(hipEventElapsedTime(&ms, e0, e1));
+  CHECK(hipEventDestroy(e0)); CHECK(hipEventDestroy(e1));
   return ms / reps;
+}
+
+// Each instruction is timed at three launch shapes -- one round of 32 waves per CU repeated 5
+// times, and single launches of 8,192 and 16,384 blocks (tools/csqr_bench.hip's shape) -- and
+// the JSON gives every rate and the best ("<instr>_Tops").  bench.py prices the integer-VALU
+// roofline with these and takes as the v_mad_u64_u32 peak the larger of the best rate and the
+// issue-model bound of 39.3 T/s (256 CU x 4 SIMD x 16 lanes/clk x 2.4 GHz for a 4-cycle op).
+struct Shape { int blocks, reps; };
+
+template <typename K>
+static void report(const char* name, K kern, uint64_t* d, const Shape* shapes, int ns, double ops_per_lane) {
+  double best = 0;
+  printf(", \"%s_Tops_by_shape\": [", name);
+  for (int i = 0; i < ns; ++i) {
+    const double t = time_kernel(kern, d, shapes[i].blocks, shapes[i].reps);
+    const double r = (double)shapes[i].blocks * 256.0 * ops_per_lane / (t * 1e-3) / 1e12;
+    if (r > best) best = r;
+    printf("%s{\"blocks\": %d, \"reps\": %d, \"Tops\": %.3f}", i ? ", " : "", shapes[i].blocks, shapes[i].reps, r);
+  }
+  printf("], \"%s_Tops\": %.3f", name, best);
 }
 
 int main() {
   hipDeviceProp_t p; CHECK(hipGetDeviceProperties(&p, 0));
   const int cus = p.multiProcessorCount;
-  const int blocks = cus * 8;  // 8 x 256-thread blocks per CU = 32 waves/CU
-  uint64_t* d; CHECK(hipMalloc(&d, (size_t)blocks * 256 * 8));
-  const double lanes = (double)blocks * 256.0;
-  const double ops = lanes * ITERS * 8.0;
-  double t;
+  const Shape shapes[3] = {{cus * 8, 5}, {8192, 1}, {16384, 1}};
+  const int max_blocks = 16384;
+  uint64_t* d; CHECK(hipMalloc(&d, (size_t)max_blocks * 256 * 8));
+  const double o = (double)ITERS * 8.0;   // instructions per lane
   printf("{\"device\": \"%s\", \"cus\": %d, \"clock_khz\": %d", p.gcnArchName, cus, p.clockRate);
-  t = time_kernel(k_mad64, d, blocks, 5);
-  printf(", \"v_mad_u64_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_addc, d, blocks, 5);
-  printf(", \"v_add_co+v_addc_co_Tops\": %.3f", 2.0 * ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_mullo, d, blocks, 5);
-  printf(", \"v_mul_lo_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_add, d, blocks, 5);
-  printf(", \"v_add_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_alignbit, d, blocks, 5);
-  printf(", \"v_alignbit_b32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_add3, d, blocks, 5);
-  printf(", \"v_add3_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_and, d, blocks, 5);
-  printf(", \"v_and_b32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_cndmask, d, blocks, 5);
-  printf(", \"v_cmp+v_cndmask_Tops\": %.3f", 2.0 * ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_dpp, d, blocks, 5);
-  printf(", \"v_mov_b32_dpp_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_lshl_add, d, blocks, 5);
-  printf(", \"v_lshl_add_u32_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_shr64, d, blocks, 5);
-  printf(", \"v_lshrrev_b64_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
-  t = time_kernel(k_lshladd64, d, blocks, 5);
-  printf(", \"v_lshl_add_u64_Tops\": %.3f", ops / (t * 1e-3) / 1e12);
+  report("v_mad_u64_u32", k_mad64, d, shapes, 3, o);
+  report("v_add_co+v_addc_co", k_addc, d, shapes, 3, 2 * o);
+  report("v_mul_lo_u32", k_mullo, d, shapes, 3, o);
+  report("v_add_u32", k_add, d, shapes, 3, o);
+  report("v_alignbit_b32", k_alignbit, d, shapes, 3, o);
+  report("v_add3_u32", k_add3, d, shapes, 3, o);
+  report("v_and_b32", k_and, d, shapes, 3, o);
+  report("v_cmp+v_cndmask", k_cndmask, d, shapes, 3, 2 * o);
+  report("v_mov_b32_dpp", k_dpp, d, shapes, 3, o);
+  report("v_lshl_add_u32", k_lshl_add, d, shapes, 3, o);
+  report("v_lshrrev_b64", k_shr64, d, shapes, 3, o);
+  report("v_lshl_add_u64", k_lshladd64, d, shapes, 3, o);
   printf("}\n");
   CHECK(hipFree(d));
   return 0;
