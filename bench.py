@@ -46,12 +46,21 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "consensus-specs_amd"))
 
-VALU_PEAK_FILE = os.path.join(ROOT, "profiles", "valu_peak_r02.json")
+VALU_PEAK_FILE = os.path.join(ROOT, "profiles", "valu_peak_r04.json")
 # Algorithmic work unit: one 381-bit Montgomery product = 300 32x32->64 MACs
 # (12x12 product + 12x12 reduction + 12 quotient digits at 32-bit limbs).  The
 # engine's radix-2^28 product issues 392 MACs; the excess is implementation
 # overhead and is deliberately not credited.
 MACS_PER_FP_MUL = 300
+# The op-count host build counts the 28x28-bit MACs each Fp product issues (fp_mul 392,
+# fp_sqr 301, lazy half-products 196 / 105, wide reductions 196; bls381_field.hpp
+# BLS_COUNT_MACS); Fp-product equivalents = MACs / 392, so a squaring or a lazy square
+# is credited by its products, not as a full product.
+ISSUED_MACS_PER_FP_MUL = 392
+# Integer-VALU peak: v_mad_u64_u32 issues over 4 cycles per wave64 on a SIMD (16 lanes per
+# clock; MI355X_MICROARCH.md: a full-rate VALU op takes 2), so 256 CUs x 4 SIMDs x 16 x 2.4 GHz.
+# The denominator is the larger of this bound and the best rate tools/valu_peak measures.
+MAD_ISSUE_BOUND_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 DOMAIN_DEPOSIT = 3
 
 
@@ -164,12 +173,15 @@ def make_workload(native, n, seed):
 
 
 def load_valu_peak():
+    """(peak T MAC/s, source): max(the measured best v_mad_u64_u32 rate, the 39.3 T/s issue bound)."""
     try:
         with open(VALU_PEAK_FILE) as f:
             d = json.load(f)
-        return float(d["v_mad_u64_u32_Tops"]), VALU_PEAK_FILE
+        meas = float(d["v_mad_u64_u32_Tops"])
     except Exception:
-        return None, None
+        return MAD_ISSUE_BOUND_TOPS, "issue bound (no measurement file)"
+    src = "max(issue bound %.2f, measured %.2f in %s)" % (MAD_ISSUE_BOUND_TOPS, meas, os.path.relpath(VALU_PEAK_FILE, ROOT))
+    return max(meas, MAD_ISSUE_BOUND_TOPS), src
 
 
 # profile key (bls381_profile_read) -> kernel symbol in rocprofv3 / PMC output
@@ -204,10 +216,9 @@ def load_pmc_traffic(prof_key, n):
 def issue_roofline(prof_key, n, measured_ms):
     """Instruction-issue roofline of a kernel: its VALU instructions per launch from the
     newest committed PMC pass (SQ_INSTS_VALU, _INT64, _INT32; wave instructions), each class priced at
-    its measured chip-wide issue rate (profiles/valu_peak_r02.json: v_mad_u64_u32 for INT64, v_add_u32 for
-    INT32, the median VOP3 rate for the rest), against the launch's live HIP-event time.  frac near 1
-    means the kernel issues VALU work back to back; the MAC-peak frac above is then bounded by the
-    representation (392 issued MACs per 300-MAC Fp product) and the non-MAC instructions."""
+    its best measured chip-wide issue rate from one tools/valu_peak run (VALU_PEAK_FILE: v_mad_u64_u32
+    for INT64, v_add_u32 for INT32, the median VOP3 rate for the rest), against the launch's live
+    HIP-event time.  frac < 1 is time the kernel did not issue VALU work (stalls: SQ_WAIT_ANY)."""
     import glob
     try:
         rates = json.load(open(VALU_PEAK_FILE))
@@ -237,8 +248,8 @@ def issue_roofline(prof_key, n, measured_ms):
 
 
 def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
-    """Per-stage Fp multiplications per verify, counted by the -DBLS_COUNT_OPS host build
-    (strict = 1: with the subgroup checks of BLS381_POLICY_STRICT)."""
+    """Per-stage Fp-product equivalents per verify (MACs issued / 392), counted by the -DBLS_COUNT_OPS
+    host build (strict = 1: with the subgroup checks of BLS381_POLICY_STRICT)."""
     import build_native
     path = build_native.build_hostcheck(count_ops=True)
     L = ctypes.CDLL(path)
@@ -253,7 +264,7 @@ def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
             if done == k:
                 break
     names = ["decode_g1", "decode_g2", "hash_to_g2", "miller_loop_2", "final_exp", "miller_lines", "miller_accum"]
-    return {nm: tot[j] / done for j, nm in enumerate(names)}
+    return {nm: tot[j] / done / ISSUED_MACS_PER_FP_MUL for j, nm in enumerate(names)}
 
 
 def agg_roofline(aprof, sample_pks, k, keys):
@@ -265,7 +276,7 @@ def agg_roofline(aprof, sample_pks, k, keys):
     out = ctypes.c_uint64()
     if L.hc_count_aggregate(ctypes.c_size_t(k), sample_pks, ctypes.byref(out)) != 0:
         return None
-    per_key = out.value / k
+    per_key = out.value / k / ISSUED_MACS_PER_FP_MUL
     ms = {kk: v["total_ms"] / v["count"] for kk, v in aprof.items()}
     dom = max(ms, key=ms.get)
     peak, _ = load_valu_peak()

@@ -13,16 +13,14 @@
 namespace bls381 {
 
 #if defined(BLS_COUNT_OPS) && !defined(__HIP_DEVICE_COMPILE__)
-// host op-count build (tools / bench roofline): Fp multiplications executed
-inline thread_local uint64_t g_fp_mul_count = 0;
-// lazy reduction (bls381_lazy.hpp): a 14x14 product into a wide value and a wide
-// reduction each count as half an Fp multiplication
-inline thread_local uint64_t g_fp_half_count = 0;
-#define BLS_COUNT_FP_MUL() (++g_fp_mul_count)
-#define BLS_COUNT_FP_HALF() (++g_fp_half_count)
+// host op-count build (bench.py roofline): the 28x28-bit partial products (MACs) of the
+// Fp products executed, each counted by the MACs it issues -- fp_mul 392 (196 product +
+// 196 reduction), fp_sqr 301 (105 + 196), and in the lazy forms (bls381_lazy.hpp) wmac
+// 196, wsqr_k 105, wredc 196.  bench.py divides by 392 for Fp-product equivalents.
+inline thread_local uint64_t g_fp_macs = 0;
+#define BLS_COUNT_MACS(k) (g_fp_macs += (k))
 #else
-#define BLS_COUNT_FP_MUL() ((void)0)
-#define BLS_COUNT_FP_HALF() ((void)0)
+#define BLS_COUNT_MACS(k) ((void)0)
 #endif
 #if !defined(__HIP_DEVICE_COMPILE__) && !defined(__HIP__)
 // host build: inversions that took fp_inv's fallback (tests assert none do)
@@ -298,8 +296,8 @@ BLS_NOINLINE fpv_t fp_sqr_call(fpv_t a) { return fp_pack(fp_sqr_body(fp_unpack(a
 BLS_INLINE fp_t fp_mul(const fp_t& a, const fp_t& b) { return fp_unpack(fp_mul_call(fp_pack(a), fp_pack(b))); }
 BLS_INLINE fp_t fp_sqr(const fp_t& a) { return fp_unpack(fp_sqr_call(fp_pack(a))); }
 #else
-BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) { BLS_COUNT_FP_MUL(); return fp_mul_body(a, b); }
-BLS_NOINLINE fp_t fp_sqr(fp_t a) { BLS_COUNT_FP_MUL(); return fp_sqr_body(a); }
+BLS_NOINLINE fp_t fp_mul(fp_t a, fp_t b) { BLS_COUNT_MACS(392); return fp_mul_body(a, b); }
+BLS_NOINLINE fp_t fp_sqr(fp_t a) { BLS_COUNT_MACS(301); return fp_sqr_body(a); }
 #endif
 
 // k * a for a small constant k: one reduction for k <= 8 (k a < 16q, limbs < 2^31)

@@ -36,7 +36,7 @@ BLS_INLINE void wz_init(wide_t& T) {
 
 // T += x y  (signed limbs)
 BLS_INLINE void wmac(wide_t& T, const lv_t& x, const lv_t& y) {
-  BLS_COUNT_FP_HALF();
+  BLS_COUNT_MACS(196);
 #pragma unroll
   for (int i = 0; i < 14; ++i)
 #pragma unroll
@@ -45,7 +45,7 @@ BLS_INLINE void wmac(wide_t& T, const lv_t& x, const lv_t& y) {
 
 // T += k x^2 for a small signed k (105 products: cross terms doubled in the multiplier)
 BLS_INLINE void wsqr_k(wide_t& T, const lv_t& x, int32_t k) {
-  BLS_COUNT_FP_HALF();
+  BLS_COUNT_MACS(105);
 #pragma unroll
   for (int i = 0; i < 14; ++i) {
     const int32_t d = k * x[i], c = 2 * k * x[i];
@@ -57,7 +57,7 @@ BLS_INLINE void wsqr_k(wide_t& T, const lv_t& x, int32_t k) {
 
 // signed Montgomery reduction T 2^-392 mod q (see the header for the bounds)
 BLS_INLINE fp_t wredc(wide_t& T) {
-  BLS_COUNT_FP_HALF();
+  BLS_COUNT_MACS(196);
 #pragma unroll
   for (int i = 0; i < 14; ++i) {
     const uint32_t m = ((uint32_t)T.c[i] * Q_INV28) & FP_MASK;

@@ -290,7 +290,8 @@ int hc_ssz_root(const uint8_t* item, const uint32_t* prog, uint32_t plen, uint8_
 }
 
 #if defined(BLS_COUNT_OPS)
-// Per-stage Fp-multiplication counts of one bls_verify exactly as the gfx950
+// Per-stage MAC counts (BLS_COUNT_MACS: partial products of the Fp products, 392 per
+// fp_mul) of one bls_verify exactly as the gfx950
 // kernels of bls381_capi.hip stage it (decode_g1 [+ subgroup check when strict],
 // decode_g2 [+ subgroup check], hash_to_g2, miller_loop_2, final_exp).  out[5]
 // receives the counts.
@@ -298,30 +299,30 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
                            int strict, uint64_t* out) {
   aff_t<fp_t> P;
   aff_t<fp2_t> S, H;
-  g_fp_mul_count = g_fp_half_count = 0;
+  g_fp_macs = 0;
   int sp = g1_decompress(P, pk48, !strict);
   if (strict && sp == PT_OK && !g1_in_subgroup(P)) sp = PT_BAD;
-  out[0] = g_fp_mul_count + g_fp_half_count / 2;
-  g_fp_mul_count = g_fp_half_count = 0;
+  out[0] = g_fp_macs;
+  g_fp_macs = 0;
   int ss = g2_decompress(S, sig96, !strict);
   if (strict && ss == PT_OK && !g2_in_subgroup(S)) ss = PT_BAD;
-  out[1] = g_fp_mul_count + g_fp_half_count / 2;
-  g_fp_mul_count = g_fp_half_count = 0;
+  out[1] = g_fp_macs;
+  g_fp_macs = 0;
   aff_t<fp2_t> c;
   hash_to_g2_candidate(c, msg32, 32, dom8);
   jac_to_aff(H, g2_mul_bp(c));
-  out[2] = g_fp_mul_count + g_fp_half_count / 2;
+  out[2] = g_fp_macs;
   if (sp != PT_OK || ss != PT_OK) { out[3] = out[4] = 0; return -1; }
-  g_fp_mul_count = g_fp_half_count = 0;
+  g_fp_macs = 0;
   aff_t<fp2_t> Q[2] = {S, H};
   aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
   g1_line_pre Pp[2] = {g1_prepare(ng), g1_prepare(P)};
   bool degen = false;
   const fp12_t f = miller_loop_n<2>(Q, Pp, degen);
-  out[3] = g_fp_mul_count + g_fp_half_count / 2;
-  g_fp_mul_count = g_fp_half_count = 0;
+  out[3] = g_fp_macs;
+  g_fp_macs = 0;
   const bool ok = fp12_is_one(final_exp(f));
-  out[4] = g_fp_mul_count + g_fp_half_count / 2;
+  out[4] = g_fp_macs;
   // the split Miller loop of the throughput path, per kernel (bls381_kernels.hpp):
   // out[5] k_ml_lines (both running points, L = l l'), out[6] k_ml_accum (f^2 L)
   uint64_t lines = 0, accum = 0;
@@ -331,16 +332,16 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   int step = 0;
   auto run_step = [&](bool add) {
     fp2_t c[3], d[3];
-    g_fp_mul_count = g_fp_half_count = 0;
+    g_fp_macs = 0;
     if (add) { line_add(T[0], Q[0], Pp[0], c[0], c[1], c[2]); line_add(T[1], Q[1], Pp[1], d[0], d[1], d[2]); }
     else { line_dbl(T[0], Pp[0], c[0], c[1], c[2]); line_dbl(T[1], Pp[1], d[0], d[1], d[2]); }
     const fp12_t L = line_pair_product(c[0], c[1], c[2], d[0], d[1], d[2]);
-    lines += g_fp_mul_count + g_fp_half_count / 2;
-    g_fp_mul_count = g_fp_half_count = 0;
+    lines += g_fp_macs;
+    g_fp_macs = 0;
     if (step == 0) g = L;
     else if (add || step == 1) g = fp12_mul_by_line_pair_inl(g, L);
     else g = fp12_mul_by_line_pair_inl(fp12_sqr_inl(g), L);
-    accum += g_fp_mul_count + g_fp_half_count / 2;
+    accum += g_fp_macs;
     ++step;
   };
   for (int b = 62; b >= 0; --b) {
@@ -352,9 +353,9 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   return ok ? 1 : 0;
 }
 
-// Fp multiplications of one committee aggregation of n pubkeys (decode + adds)
+// MACs (BLS_COUNT_MACS) of one committee aggregation of n pubkeys (decode + adds)
 int hc_count_aggregate(size_t n, const uint8_t* pks, uint64_t* out) {
-  g_fp_mul_count = 0;
+  g_fp_macs = 0;
   jac_t<fp_t> acc = jac_infinity<fp_t>();
   for (size_t i = 0; i < n; ++i) {
     aff_t<fp_t> a;
@@ -364,7 +365,7 @@ int hc_count_aggregate(size_t n, const uint8_t* pks, uint64_t* out) {
   }
   uint8_t b[48];
   g1_compress(b, acc);
-  *out = g_fp_mul_count;
+  *out = g_fp_macs;
   return 0;
 }
 #endif
