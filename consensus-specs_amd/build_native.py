@@ -33,9 +33,12 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
-def build_hip(force=False, extra=()):
+def build_hip(force=False, extra=(), out=None):
+    """out: another target (a measurement variant, variants/<name>/libbls381.so, built with `extra`
+    defines and selected at run time through BLS381_LIB)."""
     os.makedirs(LIB, exist_ok=True)
-    out = os.path.join(LIB, "libbls381.so")
+    out = out or os.path.join(LIB, "libbls381.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     deps = [os.path.join(CSRC, f) for f in HIP_SOURCES + HEADERS] + [os.path.join(INC, "bls381.h")]
     if not force and _newer(out, deps):
         return out

@@ -31,12 +31,32 @@ def from_db(path):
     return agg
 
 
+def from_csv(path):
+    """the same aggregation from a --output-format csv kernel trace (*_kernel_trace.csv)"""
+    import csv
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), int(r["VGPR_Count"] or 0),
+                         int(r["Accum_VGPR_Count"] or 0), int(r["Scratch_Size"] or 0), int(r["Grid_Size_X"] or 0),
+                         int(r["Workgroup_Size_X"] or 0)))
+    agg = defaultdict(lambda: {"n": 0, "tot": 0.0, "mn": 1e30, "mx": 0.0, "vgpr": 0, "scratch": 0, "grid": 0})
+    for name, dur, vg, ag, sc, gx, wx in rows:
+        a = agg[short(name)]
+        d = dur / 1e6
+        a["n"] += 1; a["tot"] += d; a["mn"] = min(a["mn"], d); a["mx"] = max(a["mx"], d)
+        a["vgpr"] = max(a["vgpr"], vg + ag); a["scratch"] = max(a["scratch"], sc)
+        a["grid"] = max(a["grid"], gx)
+    return agg
+
+
 def main():
     src = sys.argv[1]
     if os.path.isdir(src):
         dbs = glob.glob(os.path.join(src, "**", "*.db"), recursive=True)
-        src = dbs[0]
-    agg = from_db(src)
+        csvs = glob.glob(os.path.join(src, "**", "*kernel_trace.csv"), recursive=True)
+        src = dbs[0] if dbs else csvs[0]
+    agg = from_csv(src) if src.endswith(".csv") else from_db(src)
     total = sum(a["tot"] for a in agg.values())
     lines = ["| kernel | calls | avg ms | min ms | max ms | share | VGPR+AGPR | scratch B/lane | grid (lanes) |",
              "|---|---|---|---|---|---|---|---|---|"]
