@@ -191,10 +191,30 @@ PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2_1", "has
                   "hash_cand": "k_hash_cand_1", "hash_bp": "k_hash_bp"}
 # the C2 batch (2^16 items) runs the split Miller loop: the monolithic count is not part of its pipeline
 PIPELINE_STAGES = ["decode_g1", "decode_g2", "hash_to_g2", "miller_lines", "miller_accum", "final_exp"]
+# the final exponentiation of the throughput path runs as six launches (BLS_FE_SPLIT): its stage is
+# their sum; kernel symbols (PMC / rocprof names) with their launches per step
+FE_SPLIT_KEYS = ("final_exp_easy", "final_exp_pow", "final_exp_last")
+FE_SPLIT_KERNELS = [("k_fe_easy", 1), ("k_fe_pow<0>", 2), ("k_fe_pow<1>", 1), ("k_fe_pow<2>", 1), ("k_fe_last", 1)]
 
 
-def load_pmc_traffic(prof_key, n):
-    """HBM bytes per launch of the dominant kernel from the newest committed PMC pass
+def stage_times(prof, steps):
+    """ms per step of each pipeline stage from the profile (the split final exponentiation's six
+    launches summed into "final_exp")"""
+    ms = {k: v["total_ms"] / steps for k, v in prof.items() if k not in FE_SPLIT_KEYS}
+    if any(k in prof for k in FE_SPLIT_KEYS):
+        ms["final_exp"] = sum(prof[k]["total_ms"] for k in FE_SPLIT_KEYS if k in prof) / steps
+    return ms
+
+
+def stage_kernels(prof_key, prof):
+    """[(kernel symbol, launches per step)] of a stage"""
+    if prof_key == "final_exp" and "final_exp_pow" in prof:
+        return FE_SPLIT_KERNELS
+    return [(PROFILE_KERNEL[prof_key], 1)]
+
+
+def load_pmc_traffic(kernels, n):
+    """HBM bytes per step of the dominant stage's kernels ([(symbol, launches)]) from the newest committed PMC pass
     (profiles/pmc_<tag>_counters.json, written by tools/pmc_summary.py from separate rocprofv3 --pmc
     runs of tools/prof_workload.py at the same n; FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM").
     PMC counters cannot be read inside the timed run, so this is the last profiled build's figure."""
@@ -204,16 +224,19 @@ def load_pmc_traffic(prof_key, n):
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            k = d["kernels"][PROFILE_KERNEL[prof_key]]
-            if int(k.get("waves", 0)) * 64 not in (n, 2 * n):   # lanes = n (G1) or 2n (lane-pair)
-                continue
-            return k["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+            tot = 0.0
+            for sym, launches in kernels:
+                k = d["kernels"][sym]
+                if int(k.get("waves", 0)) * 64 not in (n, 2 * n):   # lanes = n (G1) or 2n (lane-pair)
+                    raise KeyError(sym)
+                tot += launches * k["hbm_bytes_per_launch"]
+            return tot, os.path.relpath(f, ROOT)
         except Exception:
             continue
     return None, None
 
 
-def issue_roofline(prof_key, n, measured_ms):
+def issue_roofline(kernels, n, measured_ms):
     """Instruction-issue roofline of a kernel: its VALU instructions per launch from the
     newest committed PMC pass (SQ_INSTS_VALU, _INT64, _INT32; wave instructions), each class priced at
     its best measured chip-wide issue rate from one tools/valu_peak run (VALU_PEAK_FILE: v_mad_u64_u32
@@ -229,14 +252,19 @@ def issue_roofline(prof_key, n, measured_ms):
     r_other = vop3[len(vop3) // 2]
     for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*_counters.json")))):
         try:
-            k = json.load(open(f))["kernels"][PROFILE_KERNEL[prof_key]]
-            if int(k.get("waves", 0)) * 64 not in (n, 2 * n) or k.get("valu_int64_insts") is None:
-                continue
-            i64, i32 = k["valu_int64_insts"], k["valu_int32_insts"]
-            other = k["valu_insts"] - i64 - i32
+            d = json.load(open(f))["kernels"]
+            i64 = i32 = allv = 0.0
+            for sym, launches in kernels:
+                k = d[sym]
+                if int(k.get("waves", 0)) * 64 not in (n, 2 * n) or k.get("valu_int64_insts") is None:
+                    raise KeyError(sym)
+                i64 += launches * k["valu_int64_insts"]
+                i32 += launches * k["valu_int32_insts"]
+                allv += launches * k["valu_insts"]
+            other = allv - i64 - i32
             model_ms = 64e3 * (i64 / (rates["v_mad_u64_u32_Tops"] * 1e12) + i32 / (rates["v_add_u32_Tops"] * 1e12) +
                                other / (r_other * 1e12))
-            return {"kernel": PROFILE_KERNEL[prof_key], "valu_int64_insts": i64, "valu_int32_insts": i32,
+            return {"kernels": [k for k, _ in kernels], "valu_int64_insts": i64, "valu_int32_insts": i32,
                     "valu_other_insts": other, "issue_time_ms": round(model_ms, 3),
                     "measured_ms": round(measured_ms, 3), "frac": round(model_ms / measured_ms, 4),
                     "rates_Tops": {"int64": rates["v_mad_u64_u32_Tops"], "int32": rates["v_add_u32_Tops"],
@@ -989,16 +1017,18 @@ def main():
 
     # ---------------- roofline of the dominant kernel (live HIP-event times)
     counts = count_fp_muls(pks, msgs, sigs, doms, strict=int(args.policy == "strict"))
-    kern_ms = {k: v["total_ms"] / v["count"] for k, v in prof.items()}
+    kern_ms = stage_times(prof, args.steps)   # ms per step of each stage (each kernel once per step)
     dom_k = max(kern_ms, key=kern_ms.get)
+    dom_kernels = stage_kernels(dom_k, prof)
     peak, peak_src = load_valu_peak()
     launch_macs = counts.get(dom_k, 0.0) * MACS_PER_FP_MUL * n
     achieved = launch_macs / (kern_ms[dom_k] * 1e-3) / 1e12
-    traffic, traffic_src = load_pmc_traffic(dom_k, n)
-    roofline = {"bound": "valu-int32", "kernel": dom_k, "achieved": round(achieved, 3),
+    traffic, traffic_src = load_pmc_traffic(dom_kernels, n)
+    roofline = {"bound": "valu-int32", "kernel": dom_k, "kernels": [k for k, _ in dom_kernels],
+                "achieved": round(achieved, 3),
                 "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
                 "frac": round(achieved / peak, 4) if peak else None, "traffic": traffic,
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
+                "traffic_unit": "HBM bytes per step of the stage's launches (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
                 "macs_per_launch": launch_macs,
                 "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
                 "peak_source": peak_src}
@@ -1007,7 +1037,7 @@ def main():
     whole = sum(counts[k] for k in PIPELINE_STAGES) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
     roofline["pipeline_achieved"] = round(whole, 3)
     roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
-    roofline["issue"] = issue_roofline(dom_k, n, kern_ms[dom_k])
+    roofline["issue"] = issue_roofline(dom_kernels, n, kern_ms[dom_k])
 
     cpu = None
     if world == 1 and not args.no_cpu_baseline:

@@ -45,9 +45,13 @@ def build_hip(force=False, extra=(), out=None):
     # built beside the target and renamed into place, so a snapshot of the tree taken while
     # hipcc runs (a GPU call) sees the old library or the new one, never a partial file
     tmp = out + ".partial"
+    import time
+    t0 = time.time()
     _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INC, "-I", CSRC,
           *extra, *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", tmp])
     os.replace(tmp, out)
+    # stamped with the time the sources were read: a source edited during the build stays newer
+    os.utime(out, (t0, t0))
     return out
 
 

@@ -226,7 +226,29 @@ bool fe_oct(size_t n) {
   static const int on = env_knob("BLS381_FE_OCT", 0);
   return on && n <= BLS_FE_OCT_MAX_N;
 }
-int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts) {
+// BLS_FE_SPLIT=1: the throughput-path final exponentiation as six launches (k_fe_easy, k_fe_pow,
+// k_fe_last) over 4 Fp12 buffers per item (fe_ws_words); 0: the one-kernel k_final_exp_verdict
+#ifndef BLS_FE_SPLIT
+#define BLS_FE_SPLIT 1
+#endif
+size_t fe_ws_words(size_t n) { return (BLS_FE_SPLIT && n > BLS_FE_QUAD_MAX_N) ? 4 * 12 * FP_LIMBS * n : 0; }
+
+// tmp: fe_ws_words(n) words for the split form (nullptr: the one-kernel form)
+int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts,
+                     uint32_t* tmp = nullptr) {
+  if (tmp && fe_ws_words(n)) {
+    const dim3 g(grid_for(2 * n)), b(KBLOCK);
+    const size_t one = 12 * FP_LIMBS * n;   // one Fp12 per item, pair SoA
+    uint32_t *T = tmp, *A = tmp + one, *A2 = tmp + 2 * one, *B = tmp + 3 * one;
+    LAUNCH("final_exp_easy", s, g, b, k_fe_easy, n, f, st, T);
+    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_CONJ>, n, (const uint32_t*)T, st, A);
+    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_CONJ>, n, (const uint32_t*)A, st, A2);
+    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_FROB1>, n, (const uint32_t*)A2, st, B);
+    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_NONE>, n, (const uint32_t*)B, st, A);
+    LAUNCH("final_exp_last", s, g, b, k_fe_last, n, (const uint32_t*)A, (const uint32_t*)B, (const uint32_t*)T, st,
+           verdicts);
+    return 0;
+  }
   if (fe_oct(n))
     LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_o<1>, n, f, st, verdicts);
   else if (n <= BLS_FE_QUAD_MAX_N)
@@ -243,7 +265,7 @@ int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* 
 
 // ----------------------------------------------------- verify_batch (C2) --
 struct VerifyWs {
-  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff, *ml_L;
+  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff, *ml_L, *fe_tmp;
   uint8_t *pk_st, *sig_st, *f_st, *ml_st;
 };
 // bls_verify batches of at most this many items run each Miller pair on its own lane
@@ -275,7 +297,8 @@ size_t verify_split_chunk(size_t n) { return verify_split(n) ? std::min<size_t>(
 size_t verify_ws_size(size_t n, bool lines = true) {
   const size_t ch = lines ? verify_split_chunk(n) : 0;
   return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
-         align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) + 1024;
+         align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) +
+         (lines ? align256(4 * fe_ws_words(n)) : 0) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n, bool lines = true) {
   Bump b(ws);
@@ -291,6 +314,7 @@ VerifyWs carve_verify(void* ws, size_t n, bool lines = true) {
   w.sig_st = b.take<uint8_t>(n);
   w.f_st = b.take<uint8_t>(verify_nf(n));
   w.koff = b.take<uint32_t>(n);
+  w.fe_tmp = lines && fe_ws_words(n) ? b.take<uint32_t>(fe_ws_words(n)) : nullptr;
   return w;
 }
 
@@ -452,7 +476,7 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
            (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st,
            sig_in_loop ? 1 : 0);
   }
-  LAUNCH_FE(s, n, w.f, w.f_st, verdicts);
+  if (int rc = launch_final_exp(s, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts, w.fe_tmp)) return rc;
   return 0;
 }
 
@@ -2650,6 +2674,8 @@ namespace {
 // (k_rb_ml_lines -> k_ml_accum), so a sub-batch has B/2 item-pair values plus its
 // signature-sum value; the split loop runs in chunks of at most RB_ML_CHUNK item pairs.
 constexpr size_t RB_ML_CHUNK = 32768;
+// the MSM's point lists hold 16-bit point numbers (2 per item): at most 2^15 items per sub-batch
+constexpr size_t RB_BATCH_MAX = 32768;
 size_t rb_slots(size_t n, size_t B) { return ((n + B - 1) / B) * (B / 2 + 1); }
 size_t rb_ml_chunk(size_t n, size_t B) { return std::min<size_t>(((n + B - 1) / B) * (B / 2), RB_ML_CHUNK); }
 size_t rb_ws_size(size_t n, size_t B) {
@@ -2662,6 +2688,9 @@ size_t rb_ws_size(size_t n, size_t B) {
   s += align256(4 * ML_L_WORDS_PER_ITEM * ch_ml) + align256(ch_ml);                     // line products
   s += 2 * (align256(12 * FPW * nslots) + align256(nslots) + align256(nslots * sizeof(agg_chunk)));
   s += 2 * align256(nb) + align256(64);
+  // the signature sums as a bucket MSM (k_rb_msm_*): list starts, point lists, buckets, windows, sums
+  s += align256(4 * nb * RB_MSM_W * (RB_MSM_D + 1)) + align256(2 * nb * RB_MSM_W * 2 * B) +
+       align256(6 * FPW * nb * RB_MSM_W * RB_MSM_D) + align256(6 * FPW * nb * RB_MSM_W) + align256(6 * FPW * nb);
   // the per-item fallback over m <= n items (verify_nf(m) can exceed verify_nf(n) by the octet path's 2 per item)
   const size_t oct = std::min<size_t>(n, BLS_ML_OCT_MAX_N);
   s += align256(4 * n) + align256(n) + verify_ws_size(n) + align256(12 * FPW * 2 * oct) + align256(2 * oct);
@@ -2729,15 +2758,36 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
     // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
     LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
-    LAUNCH("rb_scale_g2", sb, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
-           (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
+    // BLS381_RB_MSM (measurement knob): 1 (default) the sub-batch sums sum_i [r_i] sig_i as one bucket
+    // MSM per sub-batch (k_rb_msm_*); 0 a joint 32-bit ladder per item (k_rb_scale_g2) and a tree sum
+    static const int rb_msm = env_knob("BLS381_RB_MSM", 1);
     const uint32_t* sjac;
     const uint8_t* sbad;
-    size_t used = 0;
-    uint8_t* sub = b.take<uint8_t>(0);
-    if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, sb, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
-      return e;
-    b.off += used;
+    if (rb_msm) {
+      uint32_t* moff = b.take<uint32_t>(nb * RB_MSM_W * (RB_MSM_D + 1));
+      uint16_t* midx = b.take<uint16_t>(nb * RB_MSM_W * 2 * B);
+      uint32_t* mbucket = b.take<uint32_t>(6 * FP_LIMBS * nb * RB_MSM_W * RB_MSM_D);
+      uint32_t* mwin = b.take<uint32_t>(6 * FP_LIMBS * nb * RB_MSM_W);
+      uint32_t* mjac = b.take<uint32_t>(6 * FP_LIMBS * nb);
+      LAUNCH("rb_msm_sort", sb, dim3((unsigned)nb), blk, k_rb_msm_sort, n, B, (const uint8_t*)d_seed,
+             (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, moff, midx);
+      const size_t tasks = nb * RB_MSM_W * (RB_MSM_D - 1);
+      LAUNCH("rb_msm_bucket", sb, dim3(grid_for(2 * tasks)), blk, k_rb_msm_bucket, n, B, nb, (const uint32_t*)w.sig_aff,
+             (const uint32_t*)moff, (const uint16_t*)midx, mbucket);
+      LAUNCH("rb_msm_window", sb, dim3(grid_for(2 * nb * RB_MSM_W)), blk, k_rb_msm_window, nb,
+             (const uint32_t*)mbucket, mwin);
+      LAUNCH("rb_msm_combine", sb, dim3(grid_for(2 * nb)), blk, k_rb_msm_combine, nb, (const uint32_t*)mwin, mjac);
+      sjac = mjac;
+      sbad = zeros;
+    } else {
+      LAUNCH("rb_scale_g2", sb, g2, blk, k_rb_scale_g2, n, (const uint8_t*)d_seed, (const uint32_t*)w.sig_aff,
+             (const uint8_t*)w.sig_st, (const uint8_t*)w.pk_st, r2);
+      size_t used = 0;
+      uint8_t* sub = b.take<uint8_t>(0);
+      if (int e = run_agg<fp2p_t>(*plan, nb, nullptr, sub, sb, &sjac, &sbad, &used, b.left(), nullptr, 0, r2, zeros, n))
+        return e;
+      b.off += used;
+    }
     LAUNCH("agg_g2_affine", sb, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
     HIPC(hipEventRecord(c->ev_join, sb));
     HIPC(hipStreamWaitEvent(c->prio, c->ev_join, 0));
@@ -2838,7 +2888,7 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
 extern "C" {
 
 size_t bls381_verify_batch_randomized_workspace_size(size_t n, size_t batch) {
-  return (batch < 2 || batch % 2) ? 0 : rb_ws_size(n ? n : 1, batch);
+  return (batch < 2 || batch % 2 || batch > RB_BATCH_MAX) ? 0 : rb_ws_size(n ? n : 1, batch);
 }
 
 int bls381_verify_batch_randomized_device(size_t n, const uint8_t* d_pks, const uint8_t* d_msgs32,
@@ -2849,7 +2899,8 @@ int bls381_verify_batch_randomized_device(size_t n, const uint8_t* d_pks, const 
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   if (n == 0) return 0;
-  if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !seed || !d_verdicts || !d_workspace || batch < 2 || batch % 2)
+  if (!d_pks || !d_msgs32 || !d_sigs || !d_dom8s || !seed || !d_verdicts || !d_workspace || batch < 2 || batch % 2 ||
+      batch > RB_BATCH_MAX)
     return BLS381_EARG;
   return run_verify_randomized(c, n, d_pks, d_msgs32, d_sigs, d_dom8s, seed, batch, d_verdicts, d_workspace,
                                rb_ws_size(n, batch), (hipStream_t)stream, stats);
@@ -2865,7 +2916,8 @@ int bls381_verify_batch_randomized(size_t n, const uint8_t* pks, const uint8_t* 
   Ctx* c = get_ctx(&rc);
   if (!c) return rc;
   if (n == 0) return 0;
-  if (!pks || !msgs32 || !sigs || !dom8s || !seed || !verdicts_out || batch < 2 || batch % 2) return BLS381_EARG;
+  if (!pks || !msgs32 || !sigs || !dom8s || !seed || !verdicts_out || batch < 2 || batch % 2 || batch > RB_BATCH_MAX)
+    return BLS381_EARG;
   std::lock_guard<std::mutex> lk(c->mu);
   const size_t in_bytes = align256(48 * n) + align256(32 * n) + align256(96 * n) + align256(8 * n) + align256(n);
   const size_t wsb = rb_ws_size(n, batch);

@@ -713,6 +713,81 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   if (lead) verdict[i] = one ? 1 : 0;
 }
 
+// ---- the final exponentiation as six launches (the throughput path, BLS_FE_SPLIT) ----
+// f^(3(q^12-1)/r) = easy part, then the hard part (x-1)^2 (x+q) (x^2+q^2-1) + 3 of final_exp
+// (bls381_pairing.hpp), one exponentiation by x per launch with the products next to it:
+//   k_fe_easy              t = f^((q^6-1)(q^2+1))                       -> T
+//   k_fe_pow<FE_CONJ> x2   a = cyc_exp_x(u) conj(u): T -> A, A -> A2
+//   k_fe_pow<FE_FROB1>     b = cyc_exp_x(a) frob(a)                       A2 -> B
+//   k_fe_pow<FE_NONE>      y = cyc_exp_x(b)                               B -> A
+//   k_fe_last              cyc_exp_x(y) frob^2(b) conj(b) t^3 == 1        -> verdict
+// The values the chain needs again later (t, b, the launch's own input) wait in HBM as pair
+// SoA, coalesced, instead of living across the exponentiation calls of one long kernel (in
+// its scratch frame: 7.2 KB/lane and ~10 GB of spill traffic per 2^16 launch, r04b).
+enum : int { FE_CONJ = 0, FE_FROB1 = 1, FE_NONE = 2 };
+
+// Each launch's work is one non-inlined device function: its temporaries (the Fp12 values
+// handed by reference to cyc_exp_x and the products) live in a stack-pointer-relative frame.
+// (Written inline in the kernels, hipcc 7.2 stops with "Illegal instruction detected: Operand
+// has incorrect register class: V_CMP_NE_U32_e32 0, $src_private_base" -- a private-to-flat
+// pointer check on a kernel frame object.)
+__device__ __noinline__ void fe_easy_run(size_t n, size_t i, const uint32_t* __restrict__ f_in,
+                                         uint32_t* __restrict__ t_out) {
+  const fp12p_t f = soa_ld12(f_in, n, i);
+  fp12p_t t = fp12_mul_inl(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
+  t = fp12_mul_inl(fp12_frob(t, 2), t);                    // ^(q^2 + 1)
+  soa_st12(t_out, n, i, t);
+}
+
+template <int MODE>
+__device__ __noinline__ void fe_pow_run(size_t n, size_t i, const uint32_t* __restrict__ u_in,
+                                        uint32_t* __restrict__ w_out) {
+  fp12p_t w = cyc_exp_x(soa_ld12(u_in, n, i));
+  if (MODE != FE_NONE) {
+    const fp12p_t u = soa_ld12(u_in, n, i);               // re-read, not kept across the call
+    w = fp12_mul_inl(w, MODE == FE_CONJ ? fp12_conj(u) : fp12_frob(u, 1));
+  }
+  soa_st12(w_out, n, i, w);
+}
+
+__device__ __noinline__ bool fe_last_run(size_t n, size_t i, const uint32_t* __restrict__ y_in,
+                                         const uint32_t* __restrict__ b_in, const uint32_t* __restrict__ t_in) {
+  fp12p_t c = cyc_exp_x(soa_ld12(y_in, n, i));                                // b^(x^2)
+  {
+    const fp12p_t b = soa_ld12(b_in, n, i);
+    c = fp12_mul_inl(fp12_mul_inl(c, fp12_frob(b, 2)), fp12_conj(b));      // b^(x^2 + q^2 - 1)
+  }
+  const fp12p_t t = soa_ld12(t_in, n, i);
+  return fp12_is_one(fp12_mul_inl(c, fp12_mul_inl(fp12_cyclotomic_sqr(t), t)));
+}
+
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_easy(size_t n, const uint32_t* __restrict__ f_in,
+                                                     const uint8_t* __restrict__ st, uint32_t* __restrict__ t_out) {
+  const size_t i = item_index<2>();
+  if (i >= n || st[i] != ST_OK) return;
+  fe_easy_run(n, i, f_in, t_out);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_pow(size_t n, const uint32_t* __restrict__ u_in,
+                                                    const uint8_t* __restrict__ st, uint32_t* __restrict__ w_out) {
+  const size_t i = item_index<2>();
+  if (i >= n || st[i] != ST_OK) return;
+  fe_pow_run<MODE>(n, i, u_in, w_out);
+}
+
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_last(size_t n, const uint32_t* __restrict__ y_in,
+                                                     const uint32_t* __restrict__ b_in,
+                                                     const uint32_t* __restrict__ t_in,
+                                                     const uint8_t* __restrict__ st, uint8_t* __restrict__ verdict) {
+  const size_t i = item_index<2>();
+  if (i >= n) return;
+  const bool lead = !pr_odd();
+  if (st[i] != ST_OK) { if (lead) verdict[i] = 0; return; }
+  const bool one = fe_last_run(n, i, y_in, b_in, t_in);
+  if (lead) verdict[i] = one ? 1 : 0;
+}
+
 // The same verdict on a lane quad (final_exp_q: each half holds one Fp6 half of
 // f and runs half of every Fp12 step): half the per-item latency, for batches
 // that leave SIMDs idle.  Item i's f is the product of NF values NF i + k of the
@@ -863,6 +938,128 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_g2_affine(size
   if (!jac_to_aff(a, soa_jac<fp2p_t>::ld(jac, ng, g))) { if (lead) st[g] = ST_INF; return; }
   soa_st_g2(out_aff, ng, g, a);
   if (lead) st[g] = ST_OK;
+}
+
+// ---- the sub-batch signature sums S_b = sum_i [r_i] sig_i as a bucket MSM (Pippenger) ----
+// With r_i = k0 + mu k1 and phi(Q) = -psi^2(Q) = (zeta x, y) = [mu] Q on G2, S_b is a multi-
+// scalar product over the 2B points Q_i, phi(Q_i) of sub-batch b with 32-bit scalars k0_i,
+// k1_i: RB_MSM_W windows of RB_MSM_C bits.  Point p of a sub-batch is item p / 2 of it, phi
+// applied when p is odd.  An item outside the batch (bad pubkey, signature not a finite G2
+// point) has scalars 0 and never enters a bucket -- the same items k_rb_scale_g2 leaves at
+// infinity.  Per item this is ~2 x 8 x 15/16 mixed additions instead of a 32-doubling joint
+// ladder per item; the per-sub-batch bucket and window sums are shared.
+//   k_rb_msm_sort    one workgroup per sub-batch: digits, counting sort by (window, digit)
+//   k_rb_msm_bucket  one lane pair per (sub-batch, window, digit): its points summed
+//   k_rb_msm_window  one lane pair per (sub-batch, window): sum_d d B_d by running sums
+//   k_rb_msm_combine one lane pair per sub-batch: sum_w 2^(C w) S_w (Horner), Jacobian out
+constexpr int RB_MSM_C = 4, RB_MSM_W = 32 / RB_MSM_C, RB_MSM_D = 1 << RB_MSM_C;
+
+// off: per (b, w) RB_MSM_D + 1 list starts (digit d's points at [off[d], off[d+1]) of the
+// (b, w) list); idx: per (b, w) 2B point numbers (uint16: B < 2^15).  The scalars are
+// recomputed in each pass (rb_scalar: one SHA-256 compression per item).
+__device__ __forceinline__ void rb_msm_scalars(const uint8_t* seed32, const uint8_t* sig_st, const uint8_t* pk_st,
+                                               size_t i, uint32_t& k0, uint32_t& k1) {
+  k0 = k1 = 0;
+  if (pk_st[i] != ST_BAD && sig_st[i] == ST_OK) {
+    const rb_weight w = rb_scalar(seed32, i);
+    k0 = w.k0; k1 = w.k1;
+  }
+}
+
+__global__ void __launch_bounds__(KBLOCK) k_rb_msm_sort(size_t n, size_t B, const uint8_t* __restrict__ seed32,
+                                                        const uint8_t* __restrict__ sig_st,
+                                                        const uint8_t* __restrict__ pk_st,
+                                                        uint32_t* __restrict__ off, uint16_t* __restrict__ idx) {
+  __shared__ uint32_t cnt[RB_MSM_W][RB_MSM_D];
+  const size_t b = blockIdx.x, base = b * B;
+  if (base >= n) return;
+  const uint32_t m = (uint32_t)(n - base < B ? n - base : B);
+  for (uint32_t t = threadIdx.x; t < RB_MSM_W * RB_MSM_D; t += blockDim.x) cnt[t / RB_MSM_D][t % RB_MSM_D] = 0;
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+    uint32_t k[2];
+    rb_msm_scalars(seed32, sig_st, pk_st, base + t, k[0], k[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int w = 0; w < RB_MSM_W; ++w) {
+        const uint32_t d = (k[h] >> (RB_MSM_C * w)) & (RB_MSM_D - 1);
+        if (d) atomicAdd(&cnt[w][d], 1u);
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < RB_MSM_W) {
+    const int w = threadIdx.x;
+    uint32_t* o = off + (b * RB_MSM_W + w) * (RB_MSM_D + 1);
+    uint32_t run = 0;
+    o[0] = 0;
+    for (int d = 1; d < RB_MSM_D; ++d) { o[d] = run; const uint32_t c = cnt[w][d]; cnt[w][d] = run; run += c; }
+    o[RB_MSM_D] = run;
+  }
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < m; t += blockDim.x) {
+    uint32_t k[2];
+    rb_msm_scalars(seed32, sig_st, pk_st, base + t, k[0], k[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int w = 0; w < RB_MSM_W; ++w) {
+        const uint32_t d = (k[h] >> (RB_MSM_C * w)) & (RB_MSM_D - 1);
+        if (d) idx[(b * RB_MSM_W + w) * 2 * B + atomicAdd(&cnt[w][d], 1u)] = (uint16_t)(2 * t + h);
+      }
+  }
+}
+
+// bucket (b, w, d), d >= 1: the sum of its points (Jacobian SoA over nb * W * D slots;
+// slot (b W + w) D + d, digit-0 slots unused)
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_msm_bucket(size_t n, size_t B, size_t nb,
+                                                         const uint32_t* __restrict__ sig_aff,
+                                                         const uint32_t* __restrict__ off,
+                                                         const uint16_t* __restrict__ idx,
+                                                         uint32_t* __restrict__ bucket) {
+  const size_t t = item_index<2>();
+  constexpr size_t TPB = RB_MSM_W * (RB_MSM_D - 1);   // tasks per sub-batch
+  if (t >= nb * TPB) return;
+  const size_t b = t / TPB, r = t % TPB, w = r / (RB_MSM_D - 1), d = r % (RB_MSM_D - 1) + 1;
+  const uint32_t* o = off + (b * RB_MSM_W + w) * (RB_MSM_D + 1);
+  const uint16_t* li = idx + (b * RB_MSM_W + w) * 2 * B;
+  jac_t<fp2p_t> acc = jac_infinity<fp2p_t>();
+  for (uint32_t k = o[d], e = o[d + 1]; k < e; ++k) {
+    const uint32_t p = li[k];
+    aff_t<fp2p_t> Q = soa_ld_g2(sig_aff, n, b * B + (p >> 1));
+    if (p & 1u) Q.x.v = fp_mul(Q.x.v, G2_ZETA_M);   // phi(Q) = (zeta x, y)
+    acc = jac_add_aff(acc, Q);
+  }
+  soa_jac<fp2p_t>::st(bucket, nb * RB_MSM_W * RB_MSM_D, (b * RB_MSM_W + w) * RB_MSM_D + d, acc);
+}
+
+// window (b, w): sum_d d B_d = sum over d of the running sums of B_15 .. B_d
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_msm_window(size_t nb, const uint32_t* __restrict__ bucket,
+                                                         uint32_t* __restrict__ win) {
+  const size_t t = item_index<2>();
+  if (t >= nb * RB_MSM_W) return;
+  const size_t ns = nb * RB_MSM_W * RB_MSM_D;
+  jac_t<fp2p_t> run = jac_infinity<fp2p_t>(), sum = jac_infinity<fp2p_t>();
+  for (int d = RB_MSM_D - 1; d >= 1; --d) {
+    run = jac_add(run, soa_jac<fp2p_t>::ld(bucket, ns, t * RB_MSM_D + d));
+    sum = jac_add(sum, run);
+  }
+  soa_jac<fp2p_t>::st(win, nb * RB_MSM_W, t, sum);
+}
+
+// sub-batch b: S_b = sum_w 2^(C w) S_(b,w), Horner from the top window
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_msm_combine(size_t nb, const uint32_t* __restrict__ win,
+                                                          uint32_t* __restrict__ out_jac) {
+  const size_t b = item_index<2>();
+  if (b >= nb) return;
+  const size_t nw = nb * RB_MSM_W;
+  jac_t<fp2p_t> acc = soa_jac<fp2p_t>::ld(win, nw, b * RB_MSM_W + RB_MSM_W - 1);
+  for (int w = RB_MSM_W - 2; w >= 0; --w) {
+#pragma unroll 1
+    for (int k = 0; k < RB_MSM_C; ++k) acc = jac_dbl(acc);
+    acc = jac_add(acc, soa_jac<fp2p_t>::ld(win, nw, b * RB_MSM_W + w));
+  }
+  soa_jac<fp2p_t>::st(out_jac, nb, b, acc);
 }
 
 // Randomized batches, split Miller loop (the C2 kernels' layout): quad q runs the pairs

@@ -139,12 +139,14 @@ int bls381_verify_batch_device(size_t n, const uint8_t* d_pks, const uint8_t* d_
 /* Opt-in randomized batch verification of n independent bls_verify items (the
  * north star's "batched Miller loops share a single final exponentiation"; SURVEY
  * §7 "Verdict semantics under batching").  Items go in sub-batches of `batch`
- * (even, >= 2); a sub-batch passes when
+ * (even, 2 <= batch <= 32768; otherwise BLS381_EARG, and the workspace size is 0); a
+ * sub-batch passes when
  *     prod_i e(H(m_i), [r_i] pk_i) * e(sum_i [r_i] sig_i, -g1) == 1,
  * r_i = k0 + mu k1 mod r, mu = -x^2, (k1, k0) = the first 8 bytes of
  * SHA-256(seed || i) as two 32-bit words (seed: 32 caller-chosen random bytes; 2^64
- * distinct weights, applied through the endomorphisms sigma / -psi^2 as joint 32-bit
- * multiplications), with one final exponentiation.  Items of a passing sub-batch are
+ * distinct weights, applied through the endomorphisms sigma / -psi^2: [r_i] pk_i as a joint
+ * 32-bit multiplication, sum_i [r_i] sig_i as one bucket multi-scalar multiplication per
+ * sub-batch), with one final exponentiation.  Items of a passing sub-batch are
  * valid (a wrong one slips through with probability <= 2^-63); every item of a failing sub-batch,
  * and every item whose signature is outside G2, is re-verified alone by the
  * default pipeline, so verdicts are the per-item ones.  The device form takes

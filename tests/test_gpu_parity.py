@@ -1050,7 +1050,7 @@ def test_randomized_batch_matches_per_item_verdicts(native, golden, torsion, pol
         native.set_subgroup_policy("pyecc")
 
 
-@pytest.mark.parametrize("n", [4096, 65536])
+@pytest.mark.parametrize("n", [4096, 5003, 65536])
 def test_randomized_batch_clean_and_tampered(native, n):
     """n valid items: every sub-batch passes (no per-item re-verification); the same batch
     with 1/16 tampered: identical verdicts to the default pipeline, failing sub-batches
@@ -1084,8 +1084,9 @@ def test_randomized_batch_clean_and_tampered(native, n):
                                                              ctypes.c_void_p(stream.cuda_stream), st))
         return v.cpu().numpy().astype(bool), list(st)
 
-    v, st = run(sigs, 64)
-    assert v.all() and st == [n, 0, 0]
+    for B in ((64, 2, 256) if n == 5003 else (64,)):   # ragged last sub-batch; every MSM sub-batch passes
+        v, st = run(sigs, B)
+        assert v.all() and st == [n, 0, 0], B
     for i in range(5, n, 16):
         j = (i + 1) % n
         if idx[j] != idx[i]:
