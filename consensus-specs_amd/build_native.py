@@ -45,10 +45,20 @@ def build_hip(force=False, extra=(), out=None):
     # built beside the target and renamed into place, so a snapshot of the tree taken while
     # hipcc runs (a GPU call) sees the old library or the new one, never a partial file
     tmp = out + ".partial"
+    import shutil
+    import tempfile
     import time
     t0 = time.time()
-    _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", INC, "-I", CSRC,
-          *extra, *[os.path.join(CSRC, f) for f in HIP_SOURCES], "-o", tmp])
+    # hipcc reads the sources twice (device code, then host code, minutes apart): it compiles a
+    # snapshot, so an edit during the build can never pair one version's kernels with another's
+    # launch code (a kernel symbol the code object lacks)
+    with tempfile.TemporaryDirectory(prefix="bls381_build_") as snap:
+        shutil.copytree(CSRC, os.path.join(snap, "csrc"))
+        shutil.copytree(INC, os.path.join(snap, "include"))
+        scs = os.path.join(snap, "csrc")
+        _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I",
+              os.path.join(snap, "include"), "-I", scs, *extra, *[os.path.join(scs, f) for f in HIP_SOURCES],
+              "-o", tmp])
     os.replace(tmp, out)
     # stamped with the time the sources were read: a source edited during the build stays newer
     os.utime(out, (t0, t0))

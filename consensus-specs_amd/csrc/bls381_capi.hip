@@ -226,10 +226,13 @@ bool fe_oct(size_t n) {
   static const int on = env_knob("BLS381_FE_OCT", 0);
   return on && n <= BLS_FE_OCT_MAX_N;
 }
-// BLS_FE_SPLIT=1: the throughput-path final exponentiation as six launches (k_fe_easy, k_fe_pow,
-// k_fe_last) over 4 Fp12 buffers per item (fe_ws_words); 0: the one-kernel k_final_exp_verdict
+// BLS_FE_SPLIT=1 (measurement knob): the throughput-path final exponentiation as six launches
+// (k_fe_easy, k_fe_pow, k_fe_last) over 4 Fp12 buffers per item (fe_ws_words); 0 (default): the
+// one-kernel k_final_exp_verdict.  r04d: 9.99 ms per 2^16 step split against ~9.1 in one kernel --
+// each launch still carries cyc_exp_x's frame, and its own product frame (fe_pow_run 2.4 KB)
+// is as large as the values it no longer keeps.
 #ifndef BLS_FE_SPLIT
-#define BLS_FE_SPLIT 1
+#define BLS_FE_SPLIT 0
 #endif
 size_t fe_ws_words(size_t n) { return (BLS_FE_SPLIT && n > BLS_FE_QUAD_MAX_N) ? 4 * 12 * FP_LIMBS * n : 0; }
 

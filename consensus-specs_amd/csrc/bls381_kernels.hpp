@@ -448,13 +448,27 @@ __device__ __forceinline__ void quad_line_pair(const fp2p_t& x0, const fp2p_t& x
   o2 = p1;
 }
 
+// BLS_ML_L_NT=1 (default): the line products are stored non-temporally -- they stream through HBM
+// to k_ml_accum, and the lines kernel's own scratch keeps the caches.  r04e, one box, two runs each:
+// k_ml_lines 6.69 / 6.70 -> 6.59 / 6.61 ms, k_ml_accum 7.29 / 7.30 -> 7.17 / 7.25 ms.
+#ifndef BLS_ML_L_NT
+#define BLS_ML_L_NT 1
+#endif
+__device__ __forceinline__ void soa_st_L(uint32_t* __restrict__ p, size_t n, size_t i, int c, const fp_t& a) {
+#if BLS_ML_L_NT
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) __builtin_nontemporal_store(a.w[k], &p[(size_t)(c * FP_LIMBS + k) * n + i]);
+#else
+  soa_st(p, n, i, c, a);
+#endif
+}
 __device__ __forceinline__ void ml_store_L(uint32_t* __restrict__ L, size_t cnt, size_t i, int j, bool hi,
                                            const fp2p_t& o0, const fp2p_t& o1, const fp2p_t& o2) {
   const size_t col = 2 * i + (pr_odd() ? 1 : 0);
   const int c = j * ML_LC + (hi ? 3 : 0);
-  soa_st(L, 2 * cnt, col, c + 0, o0.v);
-  soa_st(L, 2 * cnt, col, c + 1, o1.v);
-  if (!hi) soa_st(L, 2 * cnt, col, c + 2, o2.v);
+  soa_st_L(L, 2 * cnt, col, c + 0, o0.v);
+  soa_st_L(L, 2 * cnt, col, c + 1, o1.v);
+  if (!hi) soa_st_L(L, 2 * cnt, col, c + 2, o2.v);
 }
 
 // the 68 steps of one half's running point, with the quad's line products written to L
