@@ -396,17 +396,29 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // 2.152 M/s (k_hash_bp 4.9-5.0 ms beside decode_g2), order 3 2.199 / 2.201 (3.4 ms).
   // Under the strict policy decode_g1 carries the G1 subgroup test (3.6 ms), and waiting for
   // it costs more than sharing the chip: order 1 2.111 / 2.113 against order 3 2.062 / 2.051
-  // (r03y).  Default: 3 for py_ecc, 1 for strict.
+  // (r03y).
+  // 4 = as 3 with decode_g2 on a second side stream, so the three one-lane launches (search +
+  // root, decode_g1, decode_g2) share the chip at once and hash_bp waits for all three: the
+  // prologue is max(2.4, 2.8, 2.3) + 3.4 ms instead of max(1.7 + 1.6, 2.2) + 3.4.  r04h, one
+  // box, four alternating pairs of 10 steps: order 3 2.151-2.191 M/s (mean 2.174), order 4
+  // 2.211-2.246 (mean 2.228), every pair won by 4.  Strict, three pairs: order 1 2.131-2.140,
+  // order 4 2.122-2.125, order 3 2.026-2.038 (decode_g1's 4 ms G1 test is the critical path).
+  // Default: 4 for py_ecc, 1 for strict.
   static const int c2_order_env = env_knob("BLS381_C2_ORDER", -1);
-  const int c2_order = c2_order_env >= 0 ? c2_order_env : (chk ? 1 : 3);
+  const int c2_order = c2_order_env >= 0 ? c2_order_env : (chk ? 1 : 4);
   hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
   if (c2_order != 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
 #if BLS_DECODE_G2_SIDE
-  // both decodes in sequence beside hash_to_G2
-  if (g2_one_lane() & 1)
-    LAUNCH("decode_g2", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
+  // both decodes in sequence beside hash_to_G2 (order 4: decode_g2 on its own side stream)
+  if (c2_order == 4 && (g2_one_lane() & 1)) {
+    HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
+    LAUNCH("decode_g2_1", c->side2, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st,
+           policy_flags(sig_in_loop ? 0 : chk));
+    HIPC(hipEventRecord(c->ev_join2, c->side2));
+  } else if (g2_one_lane() & 1)
+    LAUNCH("decode_g2_1", sd, g, b, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
   else
     LAUNCH("decode_g2", sd, g2, b, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(sig_in_loop ? 0 : chk));
   if (c2_order == 2) LAUNCH("decode_g1", sd, g, b, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
@@ -425,9 +437,10 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
   if (!wide && (g2_one_lane() & 2))
     LAUNCH("hash_to_g2", s, g, b, k_hash_g2_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
-  else if (!wide && c2_order == 3 && hash_split()) {
+  else if (!wide && (c2_order == 3 || c2_order == 4) && hash_split()) {
     LAUNCH("hash_cand", s, g, b, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+    if (c2_order == 4 && (g2_one_lane() & 1)) HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
     LAUNCH("hash_bp", s, g2, b, k_hash_bp, n, w.h_aff, (uint8_t*)nullptr);
   } else if (!wide)
     LAUNCH_HASH(s, n, msgs, 32u, doms, 8, w.h_aff, (uint8_t*)nullptr);
@@ -435,6 +448,9 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
            (const uint32_t*)w.koff, 0);
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+#if BLS_DECODE_G2_SIDE
+  if (c2_order == 4 && (g2_one_lane() & 1)) HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
+#endif
   return run_verify_pairings(n, w, verdicts, s, sig_in_loop);
 }
 
@@ -488,15 +504,24 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
 struct AggPlan {
   std::vector<std::vector<agg_chunk>> levels;   // chunks per level
 };
-constexpr uint32_t CHUNK_L1 = 4 * KBLOCK;
+// Level-1 chunks hold 1-4 rounds of one input per lane slot (KBLOCK / lanes-per-point inputs per
+// round): as few rounds as still give AGG_WG_TARGET workgroups (two waves per SIMD over the whole
+// chip), so a large single group (C4: 2^17 keys) is not summed four keys per lane on half the SIMDs.
+// CHUNK_MIN bounds the chunk count for the workspace sizes (G2 points: 64 per round).
+constexpr uint32_t CHUNK_MIN = KBLOCK / 2;
+constexpr size_t AGG_WG_TARGET = 1024;
 // level-1 chunks averaging fewer inputs than this are summed one lane per chunk (k_agg_lanes)
 constexpr size_t AGG_LANE_AVG_MAX = 8;
 constexpr uint32_t CHUNK_LN = 4 * KBLOCK;
 
-AggPlan plan_agg(size_t ng, const uint32_t* offsets) {
+AggPlan plan_agg(size_t ng, const uint32_t* offsets, int lanes_per_point = 1) {
   AggPlan p;
   std::vector<uint32_t> cur_off(offsets, offsets + ng + 1);
-  uint32_t chunk = CHUNK_L1;
+  const uint32_t per_round = KBLOCK / (uint32_t)lanes_per_point;
+  const size_t total = ng ? (size_t)offsets[ng] - offsets[0] : 0;
+  const size_t rounds = std::min<size_t>(4, std::max<size_t>(1, (total + AGG_WG_TARGET * per_round - 1) /
+                                                                     (AGG_WG_TARGET * per_round)));
+  uint32_t chunk = per_round * (uint32_t)rounds;
   bool first = true;
   while (true) {
     std::vector<agg_chunk> lv;
@@ -1160,7 +1185,7 @@ size_t vm_ws_bound_sizes(size_t n_calls, size_t n_keys, size_t mlen) {
        align256(8 * nq);
   s += align256(2 * FPW * G) + align256(G) + align256(4 * FPW * G) + align256(G) + align256(4 * G);
   // group-sum levels: chunks <= groups + keys / CHUNK per level, three levels at most below 2^27 keys
-  const size_t chunks = G + n_keys / CHUNK_L1 + 1;
+  const size_t chunks = G + n_keys / CHUNK_MIN + 1;
   s += 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks)) + 256;
   s += align256(4 * FPW * nc) + align256(nc);
   // Miller values: quads, or two pair tasks per quad on the latency path
@@ -1540,7 +1565,7 @@ static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets,
   for (size_t g = 0; g < ng; ++g)
     if (offsets[g + 1] < offsets[g]) { t_err = "offsets not monotone"; return BLS381_EARG; }
   // the chunk lists are async-copy sources: they live until the stream passes them
-  auto hold = std::make_shared<AggPlan>(plan_agg(ng, offsets));
+  auto hold = std::make_shared<AggPlan>(plan_agg(ng, offsets, is_g2 ? 2 : 1));
   const AggPlan& plan = *hold;
   const uint32_t* jac;
   const uint8_t* bad;
@@ -1557,13 +1582,13 @@ static int agg_batch_impl(Ctx* c, int is_g2, size_t ng, const uint32_t* offsets,
 }
 
 static size_t agg_ws_bytes(int is_g2, size_t ng, const uint32_t* offsets) {
-  AggPlan plan = plan_agg(ng, offsets);
+  AggPlan plan = plan_agg(ng, offsets, is_g2 ? 2 : 1);
   return agg_ws_size(plan, is_g2 ? 6 : 3);
 }
 
 size_t bls381_aggregate_pubkeys_batch_workspace_size(size_t n_groups, size_t n_pks) {
   // worst case chunking: every group splits into ceil(size/CHUNK) chunks, plus levels
-  const size_t chunks = n_groups + n_pks / CHUNK_L1 + 1;
+  const size_t chunks = n_groups + n_pks / CHUNK_MIN + 1;
   return 8192 + 3 * (align256(chunks * sizeof(agg_chunk)) + align256(chunks * 3 * FPW) + align256(chunks));
 }
 
@@ -2685,7 +2710,7 @@ size_t rb_ws_size(size_t n, size_t B) {
   const size_t nb = (n + B - 1) / B, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
   size_t s = verify_ws_size(n, false) + 4 * 65536;   // decodes + hash: no split-loop line buffer
   s += align256(2 * FPW * n) + 3 * align256(n) + align256(6 * FPW * n) + align256(n);   // R1, statuses, R2, zeros
-  const size_t ch = nb + n / CHUNK_L1 + 1;                                              // R2 sums per sub-batch
+  const size_t ch = nb + n / CHUNK_MIN + 1;                                              // R2 sums per sub-batch
   s += 3 * (align256(ch * sizeof(agg_chunk)) + align256(ch * 6 * FPW) + align256(ch));
   s += align256(4 * FPW * nb) + align256(nb);                                           // signature sums
   s += align256(4 * ML_L_WORDS_PER_ITEM * ch_ml) + align256(ch_ml);                     // line products

@@ -153,6 +153,43 @@ def test_invalid_encodings_raise_in_aggregate(native, golden, policy):
 
 
 @pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_codec_fuzz_aggregates_both_policies(native, policy):
+    """The device decoders on seeded structured encodings (tests/codec_fuzz.py: all flag
+    combinations, x >= q, x = 0, junk under b_flag, G2 real parts with top bits set), each as a
+    one-key aggregate: the oracle's bytes under the call's policy, or ValueError where its codec
+    rejects.  G1 through one batch call (one group per key, the one-lane level-1 kernel), G2 per
+    call through the shim's native entry point."""
+    from codec_fuzz import g1_encodings, g2_encodings
+    strict = policy == "strict"
+    native.set_subgroup_policy(policy)
+    try:
+        keys = g1_encodings(0xC0DEC3, 1500)
+        want = []
+        for b in keys:
+            try:
+                want.append(O.aggregate_pubkeys([b], strict).hex())
+            except ValueError:
+                want.append(None)
+        off = np.arange(len(keys) + 1, dtype=np.uint32)
+        outs, st = native.aggregate_pubkeys_batch(off, b"".join(keys))
+        got = [o.hex() if s == 0 else None for o, s in zip(outs, st)]
+        assert got == want
+        assert any(w is None for w in want) and any(w is not None for w in want)
+        for b in g2_encodings(0xC0DEC4, 300):
+            try:
+                w = O.aggregate_signatures([b], strict).hex()
+            except ValueError:
+                w = None
+            try:
+                g = native.aggregate_signatures(b).hex()
+            except ValueError:
+                g = None
+            assert g == w, (b.hex(), policy)
+    finally:
+        native.set_subgroup_policy("pyecc")
+
+
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
 def test_noncanonical_aggregates_both_policies(native, noncanon, policy):
     """bls_aggregate_pubkeys / _signatures over non-canonical encodings (bls_noncanonical.json):
     py_ecc 1.7.0's bytes under "pyecc" (e.g. [00 * 48] -> 0x80 || 00*47, the order-3 point),

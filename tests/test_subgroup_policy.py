@@ -150,6 +150,43 @@ def test_host_codecs_noncanonical(L, noncanon):
                 assert got == (want[0], want[1]), hx
 
 
+def test_host_codecs_fuzz(L):
+    """Both host-built decoders against the oracle's codecs on seeded structured encodings
+    (tests/codec_fuzz.py: every flag combination, x >= q, x = 0, junk under b_flag, G2 real
+    parts with their own top bits set): same status and the same point, both policies."""
+    from codec_fuzz import g1_encodings, g2_encodings
+    buf = ctypes.create_string_buffer(192)
+    i48 = lambda b: int.from_bytes(b, "big")
+    seen = set()
+    for b in g1_encodings(0xC0DEC1, 2000):
+        for strict in (False, True):
+            try:
+                want = O.pubkey_to_G1(b, strict)
+                ws = 1 if want[2] == 0 else 0
+            except ValueError:
+                want, ws = None, 2
+            seen.add(("g1", strict, ws))
+            s = L.hc_g1_decompress(b, buf, 0 if strict else 1)
+            assert s == ws, (b.hex(), strict)
+            if s == 0:
+                assert (i48(buf.raw[:48]), i48(buf.raw[48:96])) == (want[0], want[1]), b.hex()
+    for b in g2_encodings(0xC0DEC2, 600):
+        for strict in (False, True):
+            try:
+                want = O.signature_to_G2(b, strict)
+                ws = 1 if want[2] == O.FQ2_ZERO else 0
+            except ValueError:
+                want, ws = None, 2
+            seen.add(("g2", strict, ws))
+            s = L.hc_g2_decompress(b, buf, 0 if strict else 1)
+            assert s == ws, (b.hex(), strict)
+            if s == 0:
+                got = ((i48(buf.raw[:48]), i48(buf.raw[48:96])), (i48(buf.raw[96:144]), i48(buf.raw[144:192])))
+                assert got == (want[0], want[1]), b.hex()
+    # every outcome (point, infinity, rejected) occurs for both groups under both codecs
+    assert len(seen) == 12, sorted(seen)
+
+
 _ASAN_RUNNER = r"""
 import ctypes, json, sys
 L = ctypes.CDLL(sys.argv[1])
