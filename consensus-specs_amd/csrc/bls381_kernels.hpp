@@ -491,6 +491,106 @@ __device__ __noinline__ void ml_lines_run(const aff_t<fp2p_t>& Q, const g1_line_
   }
 }
 
+// BLS_ML_LINES_LDS=1: the doubling steps' line constants (-3 xp, 2 yp: 28 words per lane) live in
+// LDS (14 KB per workgroup of 128 lanes), and Q and the addition steps' constants (-xp, yp) are
+// re-read from their SoA rows at each of the five addition steps.  Without it the loop keeps
+// all of them in the kernel's scratch frame (its live set is over the VGPR budget) and re-reads
+// them through flat loads at every step: most of k_ml_lines' HBM traffic beyond L itself.
+#ifndef BLS_ML_LINES_LDS
+#define BLS_ML_LINES_LDS 1
+#endif
+// BLS_ML_LINES_TLOCAL=1: the running point in the loop's own registers (written back at the
+// end) instead of the caller's frame
+#ifndef BLS_ML_LINES_TLOCAL
+#define BLS_ML_LINES_TLOCAL 1
+#endif
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// where a half's pair lives: Q (pair SoA of nq2 lanes, lane lp), P (G1 SoA of np items, item
+// ip) or, with p == nullptr, -[c] g1 (the constant G1_VGEN)
+struct ml_src {
+  const uint32_t* q;
+  size_t nq2, lp;
+  const uint32_t* p;
+  size_t np, ip;
+};
+__device__ __forceinline__ aff_t<fp2p_t> ml_src_q(const ml_src& s) {
+  aff_t<fp2p_t> Q;
+  Q.x = pr_make(soa_ld(s.q, s.nq2, s.lp, 0));
+  Q.y = pr_make(soa_ld(s.q, s.nq2, s.lp, 1));
+  return Q;
+}
+__device__ __forceinline__ aff_t<fp_t> ml_src_p(const ml_src& s) {
+  aff_t<fp_t> P;
+  if (s.p) {
+    P = soa_ld_g1(s.p, s.np, s.ip);
+  } else {
+    P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
+  }
+  return P;
+}
+// this lane's column of the LDS line constants: word k of -3 xp at col[k KBLOCK], of 2 yp at
+// col[(14 + k) KBLOCK] (lane-major: conflict-free)
+struct g1_dbl_lds { const lds_u32* col; };
+__device__ __forceinline__ fp_t pre_n3x(const g1_dbl_lds& p) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = p.col[k * KBLOCK];
+  return r;
+}
+__device__ __forceinline__ fp_t pre_y2(const g1_dbl_lds& p) {
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = p.col[(FP_LIMBS + k) * KBLOCK];
+  return r;
+}
+constexpr int ML_LDS_WORDS = 2 * FP_LIMBS * KBLOCK;
+__device__ __forceinline__ void ml_lds_put(lds_u32* col, const g1_line_pre& pre) {
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) {
+    col[k * KBLOCK] = pre.n3x.w[k];
+    col[(FP_LIMBS + k) * KBLOCK] = pre.y2.w[k];
+  }
+}
+// src by value: the L stores cannot alias it (a by-reference src would be re-read from the
+// caller's frame after every store)
+__device__ __noinline__ void ml_lines_run_lds(const ml_src src, const lds_u32* col, bool active,
+                                             uint32_t* __restrict__ L, size_t cnt, size_t li, g2_proj<fp2p_t>& T_out) {
+  const bool hi = qd_hi();
+  const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
+#if BLS_ML_LINES_TLOCAL
+  g2_proj<fp2p_t> T;
+#else
+  g2_proj<fp2p_t>& T = T_out;
+#endif
+  {
+    const aff_t<fp2p_t> Q = ml_src_q(src);
+    T.x = Q.x; T.y = Q.y; T.z = one;
+  }
+  const g1_dbl_lds dp{col};
+  int j = 0;
+  for (int b = 62; b >= 0; --b) {
+    fp2p_t c0, c1, c2, o0, o1, o2;
+    line_dbl(T, dp, c0, c1, c2);
+    quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
+    ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
+    if ((BLS_X_ABS >> b) & 1) {
+      const aff_t<fp2p_t> Q = ml_src_q(src);
+      const aff_t<fp_t> P = ml_src_p(src);
+      g1_line_pre pre;
+      pre.nx = fp_neg(P.x);
+      pre.y = P.y;
+      pre.n3x = pre.nx;   // unused by line_add
+      pre.y2 = P.y;
+      line_add(T, Q, pre, c0, c1, c2);
+      quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
+      ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
+    }
+  }
+#if BLS_ML_LINES_TLOCAL
+  T_out = T;
+#endif
+}
+
 // items i0 .. i0 + cnt - 1 of the batch (SoA inputs of n items); L and st_out are chunk-local
 __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t n, size_t i0, size_t cnt,
                                                     const uint32_t* __restrict__ sig_aff,
@@ -514,6 +614,15 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
   const bool active = hi ? pk_ok : sig_ok;
   const bool use_pk = hi ? pk_ok : !sig_ok;
   const uint32_t* qsrc = use_pk ? h_aff : sig_aff;
+  g2_proj<fp2p_t> T;
+#if BLS_ML_LINES_LDS
+  __shared__ uint32_t lds_pre[ML_LDS_WORDS];
+  lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
+  const ml_src src{qsrc, 2 * n, lp, use_pk ? pk_aff : nullptr, n, i};
+  ml_lds_put(col, g1_prepare(ml_src_p(src)));   // each lane writes and reads only its own column
+  ml_lines_run_lds(src, col, active, L, cnt, li, T);
+  const aff_t<fp2p_t> Q = ml_src_q(src);
+#else
   aff_t<fp2p_t> Q;
   Q.x = pr_make(soa_ld(qsrc, 2 * n, lp, 0));
   Q.y = pr_make(soa_ld(qsrc, 2 * n, lp, 1));
@@ -524,8 +633,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
     P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
   }
   const g1_line_pre pre = g1_prepare(P);
-  g2_proj<fp2p_t> T;
   ml_lines_run(Q, pre, active, L, cnt, li, T);
+#endif
   // py_ecc's zero pairing value for a degenerate loop; the strict policy's G2 test of the
   // signature on the lo half's final point (psi(sig) == -[|x|] sig)
   bool bad = active && fp2_is_zero(T.z);
@@ -544,6 +653,70 @@ __device__ __forceinline__ fp12p_t ml_load_L(const uint32_t* __restrict__ L, siz
   r.c1.c0 = e2_zero<fp2p_t>();
   r.c1.c1 = pr_make(soa_ld(L, 2 * cnt, col, c + 3));
   r.c1.c2 = pr_make(soa_ld(L, 2 * cnt, col, c + 4));
+  return r;
+}
+
+// BLS_ML_ACCUM_LDS=1: k_ml_accum stages each step's L (5 Fp per lane) in LDS -- each lane its
+// own column, 35 KB per workgroup -- and reads every coefficient at its use, instead of holding
+// all five (70 VGPRs) beside f through the step's 29 Fp2 products.
+#ifndef BLS_ML_ACCUM_LDS
+#define BLS_ML_ACCUM_LDS 0
+#endif
+constexpr int ML_ACC_LDS_WORDS = ML_LC * FP_LIMBS * KBLOCK;
+// volatile: within one lane the compiler would otherwise forward the staged values from the
+// registers that stored them (no other lane reads the column) and drop LDS altogether
+__device__ __forceinline__ fp2p_t ml_lds_c(const lds_u32* col, int c) {
+  const volatile lds_u32* v = col;
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = v[(c * FP_LIMBS + k) * KBLOCK];
+  return pr_make(r);
+}
+// step j's L from HBM into this lane's LDS column, one coefficient at a time
+__device__ __forceinline__ void ml_stage_L(lds_u32* col, const uint32_t* __restrict__ L, size_t cnt, size_t i, int j) {
+  const size_t lane = 2 * i + (pr_odd() ? 1 : 0);
+#pragma unroll
+  for (int c = 0; c < ML_LC; ++c) {
+    const fp_t v = soa_ld(L, 2 * cnt, lane, j * ML_LC + c);
+    volatile lds_u32* d = col;
+#pragma unroll
+    for (int k = 0; k < FP_LIMBS; ++k) d[(c * FP_LIMBS + k) * KBLOCK] = v.w[k];
+  }
+}
+// fp12_mul_by_line_pair_inl (bls381_pairing.hpp) with L read from LDS at each use:
+// L = (L00 + L01 v + L02 v^2) + (L11 v + L12 v^2) w, coefficients 0..4 of the column
+__device__ __forceinline__ fp12p_t fp12_mul_by_line_pair_lds(const fp12p_t& f, const lds_u32* col) {
+  const fp6p_t& a = f.c0;
+  const fp6p_t& b = f.c1;
+  fp6p_t aP;
+  {
+    const fp2p_t t0 = fp2_mul(a.c0, ml_lds_c(col, 0));
+    const fp2p_t t1 = fp2_mul(a.c1, ml_lds_c(col, 1));
+    const fp2p_t t2 = fp2_mul(a.c2, ml_lds_c(col, 2));
+    aP.c0 = fp2_add_mul_xi(t0, fp2_sub2(fp2_mul(fp2_add_lazy(a.c1, a.c2),
+                                                fp2_add_lazy(ml_lds_c(col, 1), ml_lds_c(col, 2))), t1, t2));
+    aP.c1 = fp2_add_mul_xi(fp2_sub2(fp2_mul(fp2_add_lazy(a.c0, a.c1),
+                                            fp2_add_lazy(ml_lds_c(col, 0), ml_lds_c(col, 1))), t0, t1), t2);
+    aP.c2 = fp2_add(fp2_sub2(fp2_mul(fp2_add_lazy(a.c0, a.c2),
+                                     fp2_add_lazy(ml_lds_c(col, 0), ml_lds_c(col, 2))), t0, t2), t1);
+  }
+  fp6p_t bQ;
+  {
+    const fp2p_t t1 = fp2_mul(b.c1, ml_lds_c(col, 3));
+    const fp2p_t t2 = fp2_mul(b.c2, ml_lds_c(col, 4));
+    bQ.c0 = fp2_mul_xi(fp2_sub2(fp2_mul(fp2_add_lazy(b.c1, b.c2), fp2_add_lazy(ml_lds_c(col, 3), ml_lds_c(col, 4))),
+                                t1, t2));
+    bQ.c1 = fp2_add_mul_xi(fp2_mul(b.c0, ml_lds_c(col, 3)), t2);
+    bQ.c2 = fp2_add(fp2_mul(b.c0, ml_lds_c(col, 4)), t1);
+  }
+  fp6p_t pq;
+  pq.c0 = ml_lds_c(col, 0);
+  pq.c1 = fp2_add(ml_lds_c(col, 1), ml_lds_c(col, 3));
+  pq.c2 = fp2_add(ml_lds_c(col, 2), ml_lds_c(col, 4));
+  const fp6p_t m = fp6_mul_inl(fp6_add(a, b), pq);
+  fp12p_t r;
+  r.c0 = fp6_add_mul_by_v(aP, bQ);
+  r.c1 = fp6_sub2(m, aP, bQ);
   return r;
 }
 
@@ -566,6 +739,24 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t
   if (s == ML_ST_ONE) {
     f = fp12_one<fp2p_t>();
   } else {
+#if BLS_ML_ACCUM_LDS
+    __shared__ uint32_t lds_L[ML_ACC_LDS_WORDS];
+    lds_u32* col = (lds_u32*)lds_L + threadIdx.x;   // each lane writes and reads only its own column
+    f = ml_load_L(L, cnt, li, 0);
+    int j = 1;
+    if ((BLS_X_ABS >> 62) & 1) {
+      ml_stage_L(col, L, cnt, li, j++);
+      f = fp12_mul_by_line_pair_lds(f, col);
+    }
+    for (int b = 61; b >= 0; --b) {
+      ml_stage_L(col, L, cnt, li, j++);
+      f = fp12_mul_by_line_pair_lds(fp12_sqr_inl(f), col);
+      if ((BLS_X_ABS >> b) & 1) {
+        ml_stage_L(col, L, cnt, li, j++);
+        f = fp12_mul_by_line_pair_lds(f, col);
+      }
+    }
+#else
     f = ml_load_L(L, cnt, li, 0);
     int j = 1;
     if ((BLS_X_ABS >> 62) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
@@ -573,6 +764,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t
       f = fp12_mul_by_line_pair_inl(fp12_sqr_inl(f), ml_load_L(L, cnt, li, j++));
       if ((BLS_X_ABS >> b) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
     }
+#endif
     f = fp12_conj(f);
   }
   soa_st12(f_out, n, i, f);
@@ -1102,12 +1294,20 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(siz
   const bool active = hi ? b_ok : a_ok;
   const size_t i = (hi ? b_ok : !a_ok) ? ib : ia;
   const size_t lp = 2 * i + (pr_odd() ? 1 : 0);
+  g2_proj<fp2p_t> T;
+#if BLS_ML_LINES_LDS
+  __shared__ uint32_t lds_pre[ML_LDS_WORDS];
+  lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
+  const ml_src src{h_aff, 2 * n, lp, r1_aff, n, i};
+  ml_lds_put(col, g1_prepare(ml_src_p(src)));
+  ml_lines_run_lds(src, col, active, L, cnt, lq, T);
+#else
   aff_t<fp2p_t> Q;
   Q.x = pr_make(soa_ld(h_aff, 2 * n, lp, 0));
   Q.y = pr_make(soa_ld(h_aff, 2 * n, lp, 1));
   const g1_line_pre pre = g1_prepare(soa_ld_g1(r1_aff, n, i));
-  g2_proj<fp2p_t> T;
   ml_lines_run(Q, pre, active, L, cnt, lq, T);
+#endif
   bool bad = active && fp2_is_zero(T.z);
   bad = !qd_all(!bad);
   if (lead) st_out[lq] = bad ? ST_BAD : ST_OK;

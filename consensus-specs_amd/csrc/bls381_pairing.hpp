@@ -34,9 +34,14 @@ BLS_INLINE g1_line_pre g1_prepare(const aff_t<fp_t>& p) {
 // homogeneous-projective T on E'(Fp2)
 template <class E> struct g2_proj { E x, y, z; };
 
+// the doubling step reads only -3 xp and 2 yp, through these accessors: a kernel may keep
+// them elsewhere than in a g1_line_pre (k_ml_lines: in LDS)
+BLS_HD inline const fp_t& pre_n3x(const g1_line_pre& p) { return p.n3x; }
+BLS_HD inline const fp_t& pre_y2(const g1_line_pre& p) { return p.y2; }
+
 // doubling step: T <- 2T, returns the tangent line at the old T evaluated at P
-template <class E>
-BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E& c2) {
+template <class E, class PRE>
+BLS_HD inline void line_dbl(g2_proj<E>& T, const PRE& P, E& c0, E& c1, E& c2) {
   const E XX = fp2_sqr(T.x);
   const E YY = fp2_sqr(T.y);
   const E ZZ = fp2_sqr(T.z);
@@ -44,8 +49,8 @@ BLS_HD inline void line_dbl(g2_proj<E>& T, const g1_line_pre& P, E& c0, E& c1, E
   const E b3 = fp2_mul_small(fp2_mul_small(fp2_mul_xi(ZZ), 3), 4);   // 3 b' Z^2 = 12 xi Z^2
   const E b9 = fp2_mul_small(b3, 3);                                 // 9 b' Z^2
   c0 = fp2_sub(YY, b3);
-  c1 = fp2_mul_fp(XX, P.n3x);
-  c2 = fp2_mul_fp(YZ, P.y2);
+  c1 = fp2_mul_fp(XX, pre_n3x(P));
+  c2 = fp2_mul_fp(YZ, pre_y2(P));
   const E XY = fp2_mul(T.x, T.y);
   const E h = fp2_half(fp2_add(YY, b9));
   const E b3sq = fp2_sqr(b3);                      // 9 b'^2 Z^4
