@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4/C5 lines")
+    ap.add_argument("--secondary-timeout", type=int, default=600,
+                    help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
                     help="comma list: run only these secondary lines (deposits, randomized, c3, c4, c5, rccl, latency)")
     ap.add_argument("--rb-batch", type=str, default="64", help="randomized sub-batch sizes (comma list)")
@@ -85,6 +87,7 @@ def parse():
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
                     help="subgroup policy of the headline line (bls.SUBGROUP_POLICY)")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher test hook
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: the ranks join a gloo world, report it and exit")
     return ap.parse_args()
@@ -116,8 +119,29 @@ def launch_ranks(args):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].communicate()[0].decode()
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    # rank 0's stdout is drained on a thread; if any rank fails the others are ended (a rank left
+    # waiting in a collective for a dead peer would never return)
+    import threading
+    buf = []
+    reader = threading.Thread(target=lambda: buf.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = False
+    while any(p.poll() is None for p in procs):
+        if not failed and any(p.poll() not in (None, 0) for p in procs):
+            failed = True
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 30
+            while time.time() < deadline and any(p.poll() is None for p in procs):
+                time.sleep(0.5)
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.5)
+    reader.join(timeout=30)
+    out = (buf[0] if buf else b"").decode()
+    rcs = [p.returncode for p in procs]
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     if lines:
         print(lines[-1], flush=True)
@@ -132,6 +156,8 @@ def dry_run(args, world, rank):
     """The rank side of the launcher check: a gloo world on the CPU, no device touched."""
     import torch
     import torch.distributed as dist
+    if rank == args.dry_run_fail_rank:
+        raise SystemExit("dry run: rank %d fails before joining the world" % rank)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         got = dist.get_world_size()
@@ -932,28 +958,28 @@ def main():
     total_items = n * args.steps * world
     value = total_items / elapsed
 
-    # the same batch under the other subgroup policy (same verdicts: no torsion points in it)
-    other = None
-    if not args.no_secondary:
+    def bench_other_policy():
+        # the same batch under the other subgroup policy (same verdicts: no torsion points in it)
         pol = "strict" if args.policy == "pyecc" else "pyecc"
         native.set_subgroup_policy(pol)
-        step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
+        try:
             step()
-        torch.cuda.synchronize()
-        ot = _max_time(time.perf_counter() - t0, world, dist, dev)
-        assert np.array_equal(d_ver.cpu().numpy().astype(bool), expected), "verdict mismatch under " + pol
-        other = {"subgroup_policy": pol, "verifications_per_s": n * args.steps * world / ot,
-                 "ms_per_step": 1e3 * ot / args.steps}
-        native.set_subgroup_policy(args.policy)
+            torch.cuda.synchronize()
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            ot = _max_time(time.perf_counter() - t0, world, dist, dev)
+            assert np.array_equal(d_ver.cpu().numpy().astype(bool), expected), "verdict mismatch under " + pol
+        finally:
+            native.set_subgroup_policy(args.policy)
+        return {"subgroup_policy": pol, "verifications_per_s": n * args.steps * world / ot,
+                "ms_per_step": 1e3 * ot / args.steps}
 
-    # ---------------- committee aggregation (C3 shape), device-resident
-    agg = None
-    if not args.no_aggregate:
+    def bench_aggregation():
+        # committee aggregation (C3 shape), device-resident
         nc, cs = args.committees, args.committee_size
         # distinct committees drawn from the 2^16 generated keys (131072 member slots)
         rng = np.random.default_rng(0xB15_0003 + rank)
@@ -1002,100 +1028,142 @@ def main():
                "ms_per_step": 1e3 * at / a_steps,
                "roofline": agg_roofline(aprof, cpks[:48 * cs], cs, nc * cs)}
         agg["registry"] = bench_registry_c3(native, L, args, pks, idx, offsets, d_out, world, dist, dev, stream, t_u8)
+        return agg
 
-    sec = {}
+    # ---------------- the headline's line (rank 0): roofline of the dominant kernel from the timed
+    # steps' own HIP-event profile
+    line = None
+    if rank == 0:
+        counts = count_fp_muls(pks, msgs, sigs, doms, strict=int(args.policy == "strict"))
+        kern_ms = stage_times(prof, args.steps)   # ms per step of each stage (each kernel once per step)
+        dom_k = max(kern_ms, key=kern_ms.get)
+        dom_kernels = stage_kernels(dom_k, prof)
+        peak, peak_src = load_valu_peak()
+        launch_macs = counts.get(dom_k, 0.0) * MACS_PER_FP_MUL * n
+        achieved = launch_macs / (kern_ms[dom_k] * 1e-3) / 1e12
+        traffic, traffic_src = load_pmc_traffic(dom_kernels, n)
+        roofline = {"bound": "valu-int32", "kernel": dom_k, "kernels": [k for k, _ in dom_kernels],
+                    "achieved": round(achieved, 3),
+                    "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
+                    "frac": round(achieved / peak, 4) if peak else None, "traffic": traffic,
+                    "traffic_unit": "HBM bytes per step of the stage's launches (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
+                    "macs_per_launch": launch_macs,
+                    "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
+                    "peak_source": peak_src}
+        # the whole pipeline's work over the timed step's wall time (kernels on the side stream overlap
+        # the main stream, so the sum of kernel times would double-count them)
+        whole = sum(counts[k] for k in PIPELINE_STAGES) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
+        roofline["pipeline_achieved"] = round(whole, 3)
+        roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
+        roofline["issue"] = issue_roofline(dom_kernels, n, kern_ms[dom_k])
+        line = {
+            "metric": "BLS sig verifications/sec (whole node)",
+            "value": round(value, 2),
+            "unit": "verifications/s",
+            "n_gpus": world,
+            "rccl_world": dist.get_world_size() if world > 1 else 1,
+            "rank_ms_per_step": [round(x, 3) for x in rank_ms],
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (381-bit Montgomery, 14x28-bit limbs in u32 words)",
+            "data": "synthetic (random keys/messages, signatures made on device)",
+            "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
+                       "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world,
+                       "subgroup_policy": args.policy},
+            "roofline": roofline,
+        }
+
+    # ---------------- secondary lines (other policy, C3 aggregation, deposits, randomized, C3-C5,
+    # RCCL, latency), after the headline and guarded: an error is recorded in the line instead of
+    # losing it.  With several ranks a rank that fails inside a collective would leave the others
+    # waiting in it, so any error ends the phase, and a watchdog on every rank ends it after
+    # --secondary-timeout s: rank 0 prints the headline with the lines that finished, every rank
+    # exits 0.
+    sec = {"other_policy": None, "cpu_baseline": None, "cpu_baseline_cpp": None, "aggregation": None}
+    import threading
+    state = {"printed": False}
+    emit_lock = threading.Lock()
+
+    def emit(extra=None):
+        with emit_lock:
+            if rank == 0 and not state["printed"]:
+                state["printed"] = True
+                out = dict(line)
+                out.update(sec)
+                out.update(extra or {})
+                print(json.dumps(out), flush=True)
+
+    def stop_phase(msg):
+        emit({"secondary_error": msg})
+        sys.stdout.flush()
+        sys.stderr.write("bench.py rank %d: %s\n" % (rank, msg))
+        os._exit(0)
+
+    watchdog = None
+    if world > 1:
+        watchdog = threading.Timer(args.secondary_timeout, stop_phase,
+                                   ["secondary lines stopped by the %d s watchdog" % args.secondary_timeout])
+        watchdog.daemon = True
+        watchdog.start()
+
+    def guarded(key, fn):
+        try:
+            r = fn()
+            if r is not None:
+                sec[key] = r
+        except Exception as ex:   # noqa: BLE001 -- recorded in the line
+            msg = "%s: %s: %s" % (key, type(ex).__name__, ex)
+            if world > 1:
+                stop_phase(msg)
+            sec[key] = {"error": msg}
+
     only = set(x for x in args.sections.split(",") if x)
     want = lambda k: (not args.no_secondary and not only) or k in only
+    if not args.no_secondary:
+        guarded("other_policy", bench_other_policy)
+    if not args.no_aggregate:
+        guarded("aggregation", bench_aggregation)
     if want("deposits"):
-        sec["c2_deposits"] = bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8)
+        guarded("c2_deposits", lambda: bench_deposits(native, L, args, pks, sk_ints, world, dist, dev, stream, t_u8))
     if want("randomized"):
-        sec["c2_randomized_batch"] = bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, dist,
-                                                      dev, stream, t_u8)
+        guarded("c2_randomized_batch", lambda: bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world,
+                                                                dist, dev, stream, t_u8))
     if want("c3"):
-        sec["c3_epoch"] = bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist)
+        guarded("c3_epoch", lambda: bench_c3(native, L, args, pks, sk_ints, world, rank, dev, stream, t_u8, dist))
     if want("c4"):
-        sec["c4_aggregate"] = bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist)
+        guarded("c4_aggregate", lambda: bench_c4(native, L, args, world, rank, dev, stream, t_u8, dist))
     if want("c5"):
-        sec["c5_multi_pairing"] = bench_c5(native, args, world, rank, dist, dev)
+        guarded("c5_multi_pairing", lambda: bench_c5(native, args, world, rank, dist, dev))
     if want("rccl"):
-        sec["native_rccl"] = bench_native_comm(native, args, world, rank, dist, dev)
+        guarded("native_rccl", lambda: bench_native_comm(native, args, world, rank, dist, dev))
     if want("latency") and rank == 0:
-        sec["latency"] = bench_latency(native, pks, msgs, sigs, expected)
+        guarded("latency", lambda: bench_latency(native, pks, msgs, sigs, expected))
+    if watchdog is not None:
+        watchdog.cancel()
 
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            rate, res, dt = cpu_baseline(pks, msgs, sigs, args.cpu_sample, args.cpu_procs)
+            assert list(res) == list(expected[:args.cpu_sample]), "CPU oracle disagrees with GPU verdicts"
+            sec["cpu_baseline"] = {
+                "value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
+                "sample": "first %d items of the same C2 batch, oracle/bls_oracle.py verify (py_ecc 1.7.0 "
+                          "algorithm restatement: Fq12-coordinate Miller loop, naive final exponentiation), "
+                          "multiprocessing.Pool(%d), %.1f s wall" % (args.cpu_sample, args.cpu_procs, dt)}
+            k = min(args.cpp_sample, n)
+            rate, res, dt = cpu_baseline_cpp(pks[:48 * k], msgs[:32 * k], sigs[:96 * k], doms[:8 * k], k, args.cpu_procs)
+            assert res == list(expected[:k]), "C++ host build disagrees with GPU verdicts"
+            sec["cpu_baseline_cpp"] = {
+                "value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
+                "sample": "first %d items of the same C2 batch, C++ host build of the engine's arithmetic headers "
+                          "(g++ -O2, host_check.cpp hc_verify_batch_mt), %d std::threads, %.1f s wall"
+                          % (k, args.cpu_procs, dt)}
 
-    # ---------------- roofline of the dominant kernel (live HIP-event times)
-    counts = count_fp_muls(pks, msgs, sigs, doms, strict=int(args.policy == "strict"))
-    kern_ms = stage_times(prof, args.steps)   # ms per step of each stage (each kernel once per step)
-    dom_k = max(kern_ms, key=kern_ms.get)
-    dom_kernels = stage_kernels(dom_k, prof)
-    peak, peak_src = load_valu_peak()
-    launch_macs = counts.get(dom_k, 0.0) * MACS_PER_FP_MUL * n
-    achieved = launch_macs / (kern_ms[dom_k] * 1e-3) / 1e12
-    traffic, traffic_src = load_pmc_traffic(dom_kernels, n)
-    roofline = {"bound": "valu-int32", "kernel": dom_k, "kernels": [k for k, _ in dom_kernels],
-                "achieved": round(achieved, 3),
-                "peak": peak, "unit": "T MAC/s (v_mad_u64_u32, 32x32+64)",
-                "frac": round(achieved / peak, 4) if peak else None, "traffic": traffic,
-                "traffic_unit": "HBM bytes per step of the stage's launches (PMC FETCH_SIZE x2 + WRITE_SIZE)", "traffic_source": traffic_src,
-                "macs_per_launch": launch_macs,
-                "fp_mul_per_item": counts, "kernel_avg_ms": kern_ms,
-                "peak_source": peak_src}
-    # the whole pipeline's work over the timed step's wall time (kernels on the side stream overlap
-    # the main stream, so the sum of kernel times would double-count them)
-    whole = sum(counts[k] for k in PIPELINE_STAGES) * MACS_PER_FP_MUL * n / (elapsed / args.steps) / 1e12
-    roofline["pipeline_achieved"] = round(whole, 3)
-    roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
-    roofline["issue"] = issue_roofline(dom_kernels, n, kern_ms[dom_k])
-
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        rate, res, dt = cpu_baseline(pks, msgs, sigs, args.cpu_sample, args.cpu_procs)
-        assert list(res) == list(expected[:args.cpu_sample]), "CPU oracle disagrees with GPU verdicts"
-        cpu = {"value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
-               "sample": "first %d items of the same C2 batch, oracle/bls_oracle.py verify (py_ecc 1.7.0 "
-                         "algorithm restatement: Fq12-coordinate Miller loop, naive final exponentiation), "
-                         "multiprocessing.Pool(%d), %.1f s wall" % (args.cpu_sample, args.cpu_procs, dt)}
-
-    cpu_cpp = None
-    if world == 1 and not args.no_cpu_baseline:
-        k = min(args.cpp_sample, n)
-        rate, res, dt = cpu_baseline_cpp(pks[:48 * k], msgs[:32 * k], sigs[:96 * k], doms[:8 * k], k, args.cpu_procs)
-        assert res == list(expected[:k]), "C++ host build disagrees with GPU verdicts"
-        cpu_cpp = {"value": round(rate, 3), "unit": "verifications/s", "cores": args.cpu_procs, "kind": "port",
-                   "sample": "first %d items of the same C2 batch, C++ host build of the engine's arithmetic headers "
-                             "(g++ -O2, host_check.cpp hc_verify_batch_mt), %d std::threads, %.1f s wall"
-                             % (k, args.cpu_procs, dt)}
-
-    line = {
-        "metric": "BLS sig verifications/sec (whole node)",
-        "value": round(value, 2),
-        "unit": "verifications/s",
-        "n_gpus": world,
-        "rccl_world": dist.get_world_size() if world > 1 else 1,
-        "rank_ms_per_step": [round(x, 3) for x in rank_ms],
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u32 (381-bit Montgomery, 14x28-bit limbs in u32 words)",
-        "data": "synthetic (random keys/messages, signatures made on device)",
-        "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
-                   "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world,
-                   "subgroup_policy": args.policy},
-        "other_policy": other,
-        "roofline": roofline,
-        "cpu_baseline": cpu,
-        "cpu_baseline_cpp": cpu_cpp,
-        "aggregation": agg,
-    }
-    line.update(sec)
-    print(json.dumps(line))
+        emit()
     if world > 1:
         dist.destroy_process_group()
 

@@ -33,3 +33,14 @@ def test_launcher_one_rank_dry_run():
 def test_world_size_must_match_gpus():
     r = _bench(["--gpus", "2", "--dry-run"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_launcher_ends_the_other_ranks_when_one_fails():
+    """A rank that dies leaves its peers waiting in the rendezvous: the launcher ends them and fails
+    instead of hanging (the driver's scaling run must not wait on a dead world)."""
+    import time
+    t0 = time.time()
+    r = _bench(["--gpus", "3", "--dry-run", "--dry-run-fail-rank", "1"])
+    assert r.returncode != 0
+    assert "rank exit codes" in r.stderr
+    assert time.time() - t0 < 120
