@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4/C5 lines")
-    ap.add_argument("--secondary-timeout", type=int, default=600,
+    ap.add_argument("--secondary-timeout", type=int, default=360,
                     help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
                     help="comma list: run only these secondary lines (deposits, randomized, c3, c4, c5, rccl, latency)")
