@@ -44,6 +44,10 @@ constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 #ifndef BLS_FE_WAVES_PER_EU
 #define BLS_FE_WAVES_PER_EU BLS_WAVES_PER_EU
 #endif
+// aggregation kernels (k_agg_chunks, k_agg_lanes): measurement knob
+#ifndef BLS_AGG_WAVES_PER_EU
+#define BLS_AGG_WAVES_PER_EU BLS_WAVES_PER_EU
+#endif
 
 // ------------------------------------------------------------ SoA access --
 __device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
@@ -1440,7 +1444,7 @@ __device__ __forceinline__ void agg_accumulate(jac_t<F>& acc, bool& bad, uint32_
 // chunks average a few inputs (bls_verify_multiple's per-message groups, often
 // one key each), where a workgroup per chunk would leave 127 of 128 lanes idle.
 template <int MODE>
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_lanes(size_t nchunks, const agg_chunk* __restrict__ chunks,
+__global__ void __launch_bounds__(KBLOCK, BLS_AGG_WAVES_PER_EU) k_agg_lanes(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                      const uint8_t* __restrict__ in_bytes,
                                                      uint32_t* __restrict__ out_jac, uint8_t* __restrict__ out_bad,
                                                      agg_reg_src reg, int check) {
@@ -1455,7 +1459,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_lanes(size_t n
 }
 
 template <class F, int MODE>
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
+__global__ void __launch_bounds__(KBLOCK, BLS_AGG_WAVES_PER_EU) k_agg_chunks(size_t nchunks, const agg_chunk* __restrict__ chunks,
                                                       const uint8_t* __restrict__ in_bytes,
                                                       const uint32_t* __restrict__ in_jac, size_t n_in,
                                                       const uint8_t* __restrict__ in_bad,

@@ -152,6 +152,75 @@ def test_invalid_encodings_raise_in_aggregate(native, golden, policy):
         bls.SUBGROUP_POLICY = old
 
 
+def _codec_variant_cases():
+    """(pk, msg, sig) triples from valid signatures with their encodings mutated: flags cleared
+    or flipped, x + q (and G2's real part + q, which sets z2's flag bits), infinity with and
+    without junk, a changed x.  Expected verdict per policy from the oracle's decoders: True iff
+    both inputs decode to the signed points, or both to infinity (py_ecc's pairing with an
+    infinite point is 1) -- a different point fails the pairing check.  A subset is re-checked
+    with the oracle's full verify in the test."""
+    Q = O.q
+    cases = []
+    for sk in (7, 0x1234567, 0x2f3e4d5c6b7a8990a1b2c3d4e5f60718293a4b5c6d7e8f9):
+        msg = bytes([sk % 251]) * 32
+        pk, sig = O.privtopub(sk), O.sign(msg, sk, 3)
+        z = int.from_bytes(pk, "big")
+        x, fl = z & ((1 << 381) - 1), z >> 381
+        pks = [z, z & ~(1 << 383), z ^ (1 << 381), (fl << 381) | (x ^ 1), x,
+               (1 << 383) | (1 << 382), (1 << 383) | (1 << 382) | 12345, (1 << 382) | x]
+        if x + Q < (1 << 381):
+            pks += [(fl << 381) | (x + Q), ((fl & 3) << 381) | (x + Q)]
+        z1, z2 = int.from_bytes(sig[:48], "big"), int.from_bytes(sig[48:], "big")
+        x1, f1 = z1 & ((1 << 381) - 1), z1 >> 381
+        sigs = [(z1, z2), (z1 & ~(1 << 383), z2), (z1 ^ (1 << 381), z2), (z1, z2 + Q), (z1, z2 | (1 << 383)),
+                ((1 << 383) | (1 << 382), 0), ((1 << 383) | (1 << 382) | 99, 7), (z1, z2 ^ 1)]
+        if x1 + Q < (1 << 381):
+            sigs += [((f1 << 381) | (x1 + Q), z2), (((f1 & 3) << 381) | (x1 + Q), z2)]
+        enc_pk = lambda v: v.to_bytes(48, "big")
+        enc_sig = lambda t: t[0].to_bytes(48, "big") + t[1].to_bytes(48, "big")
+        combos = [(p, sigs[0]) for p in pks] + [(pks[0], t) for t in sigs[1:]]
+        combos += [(p, t) for p in pks[5:7] for t in sigs[5:7]]     # both at infinity
+        P0, S0 = O.pubkey_to_G1(pk), O.signature_to_G2(sig)
+        for p, t in combos:
+            want = {}
+            for pol in ("pyecc", "strict"):
+                try:
+                    P = O.decompress_G1(p, pol == "strict")
+                    S = O.decompress_G2(t, pol == "strict")
+                    both_inf = O.pt_is_inf(O._FqOps, P) and O.pt_is_inf(O._Fq2Ops, S)
+                    want[pol] = both_inf or (O.pt_eq(O._FqOps, P, P0) and O.pt_eq(O._Fq2Ops, S, S0))
+                except ValueError:
+                    want[pol] = False
+            cases.append((enc_pk(p), msg, enc_sig(t), want))
+    return cases
+
+
+@pytest.mark.parametrize("n", [64, 20000, (1 << 16) + 3])
+def test_verify_codec_variants_both_policies(native, n):
+    """bls_verify over mutated encodings of valid signatures (_codec_variant_cases), tiled to n
+    items so the quad, pair and split-loop layouts all see them, under both policies; a subset
+    against the oracle's full verify (py_ecc) and verify_strict."""
+    cases = _codec_variant_cases()
+    if n == 64:
+        for pk, msg, sig, want in cases[::9]:
+            assert O.verify(msg, pk, sig, 3) == want["pyecc"], pk.hex()
+            assert O.verify_strict(msg, pk, sig, 3) == want["strict"], pk.hex()
+    reps = (n + len(cases) - 1) // len(cases)
+    tiled = (cases * reps)[:n]
+    pks = b"".join(c[0] for c in tiled)
+    msgs = b"".join(c[1] for c in tiled)
+    sigs = b"".join(c[2] for c in tiled)
+    doms = (3).to_bytes(8, "big") * n
+    try:
+        for pol in ("pyecc", "strict"):
+            native.set_subgroup_policy(pol)
+            got = list(native.verify_batch(pks, msgs, sigs, doms))
+            assert got == [c[3][pol] for c in tiled], pol
+        assert any(c[3]["pyecc"] != c[3]["strict"] for c in cases)
+    finally:
+        native.set_subgroup_policy("pyecc")
+
+
 @pytest.mark.parametrize("policy", ["pyecc", "strict"])
 def test_codec_fuzz_aggregates_both_policies(native, policy):
     """The device decoders on seeded structured encodings (tests/codec_fuzz.py: all flag
