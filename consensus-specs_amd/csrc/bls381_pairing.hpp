@@ -317,6 +317,17 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 #define BLS_CYC_TAIL_GS 1
 #endif
 
+// BLS_FE_MUL_CALL=1 (measurement knob): the final exponentiation's Fp12 products as calls
+// (fp12_mul, operands through the stack) instead of inlined
+#ifndef BLS_FE_MUL_CALL
+#define BLS_FE_MUL_CALL 0
+#endif
+#if BLS_FE_MUL_CALL
+#define FE_MUL12 fp12_mul
+#else
+#define FE_MUL12 fp12_mul_inl
+#endif
+
 #if BLS_CYC_TAIL_GS
 template <class E>
 BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
@@ -335,11 +346,11 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   E inv = fp2_inv(fp2_mul(p01, fp2_mul_small(snap[2].g2, 4)));   // 1 / (d0 d1 d2)
   fp12_g<E> x = cyc_decompress(snap[2], fp2_mul(inv, p01));       // f^(2^57)
   inv = fp2_mul(inv, fp2_mul_small(snap[2].g2, 4));               // 1 / (d0 d1)
-  fp12_g<E> r = fp12_mul_inl(x, cyc_decompress(snap[1], fp2_mul(inv, d0)));
-  r = fp12_mul_inl(r, cyc_decompress(snap[0], fp2_mul(inv, d1)));
+  fp12_g<E> r = FE_MUL12(x, cyc_decompress(snap[1], fp2_mul(inv, d0)));
+  r = FE_MUL12(r, cyc_decompress(snap[0], fp2_mul(inv, d1)));
   for (int s = 3; s < 6; ++s) {
     for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) x = fp12_cyclotomic_sqr_inl(x);
-    r = fp12_mul_inl(r, x);
+    r = FE_MUL12(r, x);
   }
   return fp12_conj(r);
 }
@@ -366,7 +377,7 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
     const E is = s ? fp2_mul(inv, pre[s - 1]) : inv;
     if (s) inv = fp2_mul(inv, fp2_mul_small(snap[s].g2, 4));
     const fp12_g<E> x = cyc_decompress(snap[s], is);
-    r = (s == 5) ? x : fp12_mul_inl(r, x);
+    r = (s == 5) ? x : FE_MUL12(r, x);
   }
   return fp12_conj(r);
 }
@@ -377,15 +388,15 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
 // Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3.
 template <class E>
 BLS_HD inline fp12_g<E> final_exp(const fp12_g<E>& f) {
-  fp12_g<E> t = fp12_mul_inl(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
-  t = fp12_mul_inl(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
-  fp12_g<E> a = fp12_mul_inl(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
-  a = fp12_mul_inl(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
-  const fp12_g<E> b = fp12_mul_inl(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
+  fp12_g<E> t = FE_MUL12(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
+  t = FE_MUL12(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
+  fp12_g<E> a = FE_MUL12(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
+  a = FE_MUL12(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
+  const fp12_g<E> b = FE_MUL12(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
   const fp12_g<E> bx2 = cyc_exp_x(cyc_exp_x(b));
-  const fp12_g<E> c = fp12_mul_inl(fp12_mul_inl(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
-  const fp12_g<E> t3 = fp12_mul_inl(fp12_cyclotomic_sqr(t), t);
-  return fp12_mul_inl(c, t3);
+  const fp12_g<E> c = FE_MUL12(FE_MUL12(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
+  const fp12_g<E> t3 = FE_MUL12(fp12_cyclotomic_sqr(t), t);
+  return FE_MUL12(c, t3);
 }
 
 }  // namespace bls381
