@@ -82,7 +82,7 @@ def parse():
                     help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
                     help="comma list: run only these secondary lines (deposits, randomized, c3, c4, c5, rccl, latency)")
-    ap.add_argument("--rb-batch", type=str, default="64", help="randomized sub-batch sizes (comma list)")
+    ap.add_argument("--rb-batch", type=str, default="32", help="randomized sub-batch sizes (comma list)")
     ap.add_argument("--c4-keys", type=int, default=1 << 17, help="pubkeys per GPU in the C4 aggregation")
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
@@ -808,7 +808,7 @@ def bench_native_comm(native, args, world, rank, dist, dev):
 
 def bench_randomized(native, L, args, pks, msgs, sigs, doms, expected, world, dist, dev, stream, t_u8):
     """Opt-in randomized batch verification (bls381_verify_batch_randomized_device): sub-batches
-    of 64 items share one final exponentiation; per-item verdicts (failing sub-batches are
+    of 32 items (--rb-batch) share one final exponentiation; per-item verdicts (failing sub-batches are
     re-verified item by item).  On the clean C2 batch, and on the bench's 1/16-tampered one
     (nearly every sub-batch then fails: the fallback cost)."""
     import torch
