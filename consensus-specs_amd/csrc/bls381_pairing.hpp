@@ -317,6 +317,11 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 #define BLS_CYC_TAIL_GS 1
 #endif
 
+// BLS_FE_MARK(k): phase marks for tools/fe_phases.hip (no code in the library)
+#ifndef BLS_FE_MARK
+#define BLS_FE_MARK(k)
+#endif
+
 // BLS_FE_MUL_CALL=1 (measurement knob): the final exponentiation's Fp12 products as calls
 // (fp12_mul, operands through the stack) instead of inlined
 #ifndef BLS_FE_MUL_CALL
@@ -331,6 +336,7 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 #if BLS_CYC_TAIL_GS
 template <class E>
 BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+  BLS_FE_MARK(7);
   cyc_bc<E> snap[3];
   cyc_bc<E> g = cyc_compress(f);
   bool zero = false;
@@ -340,17 +346,22 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
     const bool zs = fp2_is_zero(g.g2);   // evaluated on both lanes of a pair
     zero = zero | zs;
   }
+  BLS_FE_MARK(0);
   if (BLS_ANY(zero)) return cyc_exp_x_gs(f);
   const E d0 = fp2_mul_small(snap[0].g2, 4), d1 = fp2_mul_small(snap[1].g2, 4);
   const E p01 = fp2_mul(d0, d1);
   E inv = fp2_inv(fp2_mul(p01, fp2_mul_small(snap[2].g2, 4)));   // 1 / (d0 d1 d2)
+  BLS_FE_MARK(1);
   fp12_g<E> x = cyc_decompress(snap[2], fp2_mul(inv, p01));       // f^(2^57)
   inv = fp2_mul(inv, fp2_mul_small(snap[2].g2, 4));               // 1 / (d0 d1)
   fp12_g<E> r = FE_MUL12(x, cyc_decompress(snap[1], fp2_mul(inv, d0)));
   r = FE_MUL12(r, cyc_decompress(snap[0], fp2_mul(inv, d1)));
+  BLS_FE_MARK(2);
   for (int s = 3; s < 6; ++s) {
     for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) x = fp12_cyclotomic_sqr_inl(x);
+    BLS_FE_MARK(3);
     r = FE_MUL12(r, x);
+    BLS_FE_MARK(4);
   }
   return fp12_conj(r);
 }
@@ -390,13 +401,16 @@ template <class E>
 BLS_HD inline fp12_g<E> final_exp(const fp12_g<E>& f) {
   fp12_g<E> t = FE_MUL12(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
   t = FE_MUL12(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
+  BLS_FE_MARK(5);
   fp12_g<E> a = FE_MUL12(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
   a = FE_MUL12(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
   const fp12_g<E> b = FE_MUL12(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
   const fp12_g<E> bx2 = cyc_exp_x(cyc_exp_x(b));
   const fp12_g<E> c = FE_MUL12(FE_MUL12(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
   const fp12_g<E> t3 = FE_MUL12(fp12_cyclotomic_sqr(t), t);
-  return FE_MUL12(c, t3);
+  const fp12_g<E> res = FE_MUL12(c, t3);
+  BLS_FE_MARK(6);
+  return res;
 }
 
 }  // namespace bls381
