@@ -573,6 +573,7 @@ __device__ __noinline__ void ml_lines_run_lds(const ml_src src, const lds_u32* c
   const g1_dbl_lds dp{col};
   int j = 0;
   for (int b = 62; b >= 0; --b) {
+    wave_balance((unsigned)b);
     fp2p_t c0, c1, c2, o0, o1, o2;
     line_dbl(T, dp, c0, c1, c2);
     quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
@@ -765,6 +766,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_accum(size_t
     int j = 1;
     if ((BLS_X_ABS >> 62) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
     for (int b = 61; b >= 0; --b) {
+      wave_balance((unsigned)b);
       f = fp12_mul_by_line_pair_inl(fp12_sqr_inl(f), ml_load_L(L, cnt, li, j++));
       if ((BLS_X_ABS >> b) & 1) f = fp12_mul_by_line_pair_inl(f, ml_load_L(L, cnt, li, j++));
     }

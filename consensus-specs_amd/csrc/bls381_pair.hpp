@@ -19,6 +19,32 @@
 // together; DPP reads the partner's registers): every predicate on an Fp2 value
 // is combined across the pair before it is returned.
 #pragma once
+#include <hip/hip_runtime.h>
+
+// BLS_WAVE_BALANCE=1 (default): the two waves a SIMD holds alternate their issue priority (s_setprio)
+// step by step in the Miller accumulation, the line loop and the final exponentiation's squarings.
+// Without it the older wave takes most issue slots and finishes first, and the younger runs its
+// remaining third alone at a lone wave's issue rate (tools/fe_phases.hip: in k_final_exp_verdict's
+// shape the older wave of every SIMD ends at 6.0 ms, the younger at 9.6).  r04y, one box, three
+// alternating rounds: 2.254-2.260 -> 2.268-2.279 M/s (k_ml_accum 7.21-7.23 -> 7.06-7.12 ms).
+#ifndef BLS_WAVE_BALANCE
+#define BLS_WAVE_BALANCE 1
+#endif
+namespace bls381 {
+__device__ __forceinline__ void wave_balance(unsigned step) {
+#if BLS_WAVE_BALANCE
+  // the wave's slot on its SIMD (HW_ID[3:0]); a scalar branch, since s_setprio ignores exec
+  const unsigned slot = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) & 1u;
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)((step + slot) & 1u));
+  if (hi) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(0);
+#else
+  (void)step;
+#endif
+}
+}  // namespace bls381
+#if BLS_WAVE_BALANCE && !defined(BLS_FE_STEP)
+#define BLS_FE_STEP(j) ::bls381::wave_balance((unsigned)(j))
+#endif
 #include "bls381_hash.hpp"
 #include "bls381_pairing.hpp"
 

@@ -321,6 +321,9 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 #ifndef BLS_FE_MARK
 #define BLS_FE_MARK(k)
 #endif
+#ifndef BLS_FE_STEP
+#define BLS_FE_STEP(j)
+#endif
 
 // BLS_FE_MUL_CALL=1 (measurement knob): the final exponentiation's Fp12 products as calls
 // (fp12_mul, operands through the stack) instead of inlined
@@ -341,7 +344,10 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
   cyc_bc<E> g = cyc_compress(f);
   bool zero = false;
   for (int s = 0; s < 3; ++s) {
-    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cyc_csqr(g);
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) {
+      g = cyc_csqr(g);
+      BLS_FE_STEP(j);
+    }
     snap[s] = g;
     const bool zs = fp2_is_zero(g.g2);   // evaluated on both lanes of a pair
     zero = zero | zs;
