@@ -78,6 +78,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-aggregate", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C4/C5 lines")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="headline: consecutive steps alternate over this many streams (independent batches)")
     ap.add_argument("--secondary-timeout", type=int, default=360,
                     help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
@@ -919,14 +921,24 @@ def main():
     dev = torch.device("cuda", local_rank)
     t_u8 = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
     d_pks, d_msgs, d_sigs, d_doms = t_u8(pks), t_u8(msgs), t_u8(sigs), t_u8(doms)
-    d_ver = torch.zeros(n, dtype=torch.uint8, device=dev)
-    ws = torch.empty(L.bls381_verify_batch_workspace_size(n), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
+    # --inflight K: consecutive steps alternate over K streams, each with its own workspace and verdict
+    # buffer, so a step's first launches need not wait for the previous step's last ones (independent
+    # batches, as a node verifying a stream of them would run them); every step still does the whole
+    # pipeline over its batch and every step's verdicts are checked below
+    kin = max(1, args.inflight)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(kin - 1)]
+    wss = [torch.empty(L.bls381_verify_batch_workspace_size(n), dtype=torch.uint8, device=dev) for _ in range(kin)]
+    vers = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(kin)]
+    d_ver, ws = vers[0], wss[0]
+    counter = [0]
 
     def step():
+        j = counter[0] % kin
+        counter[0] += 1
         rc = L.bls381_verify_batch_device(n, d_pks.data_ptr(), d_msgs.data_ptr(), d_sigs.data_ptr(),
-                                          d_doms.data_ptr(), d_ver.data_ptr(), ws.data_ptr(),
-                                          ctypes.c_void_p(stream.cuda_stream))
+                                          d_doms.data_ptr(), vers[j].data_ptr(), wss[j].data_ptr(),
+                                          ctypes.c_void_p(streams[j].cuda_stream))
         native.check(rc)
 
     for _ in range(args.warmup):
@@ -934,6 +946,9 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    torch.cuda.synchronize()
+    for v in vers:
+        v.zero_()
     torch.cuda.synchronize()
     native.profile_enable(True)
     t0 = time.perf_counter()
@@ -945,9 +960,11 @@ def main():
         dist.barrier()
     prof = native.profile_read()
     native.profile_enable(False)
-    got = d_ver.cpu().numpy().astype(bool)
-    if not np.array_equal(got, expected):
-        raise SystemExit("verdict mismatch on rank %d: %d wrong" % (rank, int((got != expected).sum())))
+    for j, v in enumerate(vers[:min(kin, args.steps)]):
+        got = v.cpu().numpy().astype(bool)
+        if not np.array_equal(got, expected):
+            raise SystemExit("verdict mismatch on rank %d (stream %d): %d wrong" % (rank, j, int((got != expected).sum())))
+    counter[0] = 0
     rank_ms = [1e3 * elapsed / args.steps]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -1073,6 +1090,7 @@ def main():
             "data": "synthetic (random keys/messages, signatures made on device)",
             "config": {"workload": "C2: %d independent bls_verify deposit PoP checks per GPU (domain=3, 1/16 tampered)" % n,
                        "global_batch": n * world, "parallelism": "dp%d (independent items, no collective)" % world,
+                       "batches_in_flight": kin,
                        "subgroup_policy": args.policy},
             "roofline": roofline,
         }
