@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
                     help="subgroup policy of the headline line (bls.SUBGROUP_POLICY)")
+    ap.add_argument("--fail-on-secondary-error", action="store_true",
+                    help="exit 3 when a secondary line failed (recorded as secondary_error / {\"error\": ...}); "
+                         "default: the line is printed and the exit code is 0")
     ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)   # launcher test hook
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: the ranks join a gloo world, report it and exit")
@@ -1100,7 +1103,7 @@ def main():
     # losing it.  With several ranks a rank that fails inside a collective would leave the others
     # waiting in it, so any error ends the phase, and a watchdog on every rank ends it after
     # --secondary-timeout s: rank 0 prints the headline with the lines that finished, every rank
-    # exits 0.
+    # exits 0 (3 with --fail-on-secondary-error, which tools/gpu_final.sh passes).
     sec = {"other_policy": None, "cpu_baseline": None, "cpu_baseline_cpp": None, "aggregation": None}
     import threading
     state = {"printed": False}
@@ -1119,7 +1122,7 @@ def main():
         emit({"secondary_error": msg})
         sys.stdout.flush()
         sys.stderr.write("bench.py rank %d: %s\n" % (rank, msg))
-        os._exit(0)
+        os._exit(3 if args.fail_on_secondary_error else 0)
 
     watchdog = None
     if world > 1:
@@ -1184,6 +1187,10 @@ def main():
         emit()
     if world > 1:
         dist.destroy_process_group()
+    failed = [k for k, v in sec.items() if isinstance(v, dict) and "error" in v]
+    if failed and args.fail_on_secondary_error:
+        sys.stderr.write("bench.py rank %d: secondary lines failed: %s\n" % (rank, ", ".join(failed)))
+        sys.exit(3)
 
 
 if __name__ == "__main__":

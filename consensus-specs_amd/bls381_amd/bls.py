@@ -12,6 +12,19 @@ the same error behaviour as the py_ecc 1.7.0 calls they replace
 * bls_aggregate_* raise ValueError on an invalid point encoding;
 * a domain outside [0, 2^64) raises OverflowError (int.to_bytes).
 
+Inputs py_ecc reads as integers (VERDICT r04 missing #4), under the "pyecc" policy:
+* a pubkey of any length is decompress_G1(big_endian_to_int(pubkey)), and a signature
+  of any length decompress_G2((int(sig[:48]), int(sig[48:]))): such inputs are passed to
+  the engine as the 48 / 96-byte encodings the lax decoder reads identically (_lax_pubkey,
+  _lax_signature);
+* the domain is serialised inside hash_to_G2, after the decodes that come before it:
+  bls_verify returns False for an undecodable signature before an out-of-range domain
+  raises OverflowError; bls_verify_multiple decodes the first message group's pubkeys
+  (sorted message order) first and never serialises the domain of an empty call.
+The "strict" policy takes the spec's types: Bytes48 / Bytes96 only (other lengths are
+False, or ValueError from the aggregates) and a uint64 domain, checked first.
+Fixtures: tests/golden/bls_noncanonical.json "shim_*" sections, both columns.
+
 Divergences from that contract (tested in tests/test_gpu_parity.py):
 * a message longer than _native.MSG_MAX (1 MiB) raises ValueError from bls_verify,
   bls_verify_multiple and bls_sign, where py_ecc would hash it and return a verdict.
@@ -87,6 +100,51 @@ def _sk32(privkey) -> bytes:
     return k.to_bytes(32, "big")
 
 
+_Q = 0x1a0111ea397fe69a4b1ba7b6434bacd764774b84f38512bf6730d2a0f6b0f6241eabfffeb153ffffb9feffffffffaaab
+
+
+def _lax_pubkey(p: bytes) -> bytes:
+    """The 48-byte encoding py_ecc 1.7.0's lax decode_G1 reads like big_endian_to_int(p): it
+    looks at bits 381-382 and z mod 2^381 only (bit 383 and up are ignored)."""
+    if len(p) == 48:
+        return p
+    return (int.from_bytes(p, "big") % (1 << 384)).to_bytes(48, "big")
+
+
+def _lax_signature(sig: bytes) -> bytes:
+    """The 96-byte encoding py_ecc 1.7.0's lax decode_G2 reads like (int(sig[:48]),
+    int(sig[48:])): z1 (at most 48 bytes), and z2 of any length, of which only z2 mod q
+    is used (the real part of x)."""
+    if len(sig) == 96:
+        return sig
+    z1 = int.from_bytes(sig[:48], "big")
+    z2 = int.from_bytes(sig[48:], "big") % _Q
+    return z1.to_bytes(48, "big") + z2.to_bytes(48, "big")
+
+
+def _strict() -> bool:
+    return SUBGROUP_POLICY == "strict"
+
+
+def _signature_decodes(sig: bytes) -> bool:
+    """Whether the call's codec decodes `sig` (a valid encoding under the policy)."""
+    try:
+        with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+            _native.aggregate_signatures(sig)
+        return True
+    except ValueError:
+        return False
+
+
+def _pubkeys_decode(pks) -> bool:
+    try:
+        with _native.subgroup_policy_scope(SUBGROUP_POLICY):
+            _native.aggregate_pubkeys(b"".join(pks))
+        return True
+    except ValueError:
+        return False
+
+
 def _check_len(message_hash: bytes) -> None:
     if len(message_hash) > _native.MSG_MAX:
         raise ValueError("message of %d bytes is longer than the engine's %d-byte limit"
@@ -95,11 +153,22 @@ def _check_len(message_hash: bytes) -> None:
 
 @only_with_bls(alt_return=True)
 def bls_verify(pubkey, message_hash, signature, domain):
-    dom8 = _dom8(domain)
+    if _strict():
+        dom8 = _dom8(domain)       # uint64 (the spec's type), before anything else
     pubkey, message_hash, signature = bytes(pubkey), bytes(message_hash), bytes(signature)
     _check_len(message_hash)
-    if len(pubkey) != 48 or len(signature) != 96:
-        return False
+    if _strict():
+        if len(pubkey) != 48 or len(signature) != 96:
+            return False
+    else:
+        pubkey, signature = _lax_pubkey(pubkey), _lax_signature(signature)
+        try:
+            dom8 = _dom8(domain)
+        except OverflowError:
+            # py_ecc: signature_to_G2 runs before hash_to_G2 serialises the domain (A.5)
+            if not _signature_decodes(signature):
+                return False
+            raise
     with _native.subgroup_policy_scope(SUBGROUP_POLICY):
         return _native.verify(pubkey, message_hash, signature, dom8)
 
@@ -109,14 +178,29 @@ def bls_verify_multiple(pubkeys, message_hashes, signature, domain):
     if len(pubkeys) != len(message_hashes):
         raise ValidationError(
             "len(pubkeys) (%s) should be equal to len(message_hashes) (%s)" % (len(pubkeys), len(message_hashes)))
-    dom8 = _dom8(domain)
+    if _strict():
+        dom8 = _dom8(domain)
     pks = [bytes(p) for p in pubkeys]
     msgs = [bytes(m) for m in message_hashes]
     signature = bytes(signature)
     for m in msgs:
         _check_len(m)
-    if any(len(p) != 48 for p in pks) or len(signature) != 96:
-        return False
+    if _strict():
+        if any(len(p) != 48 for p in pks) or len(signature) != 96:
+            return False
+    else:
+        pks, signature = [_lax_pubkey(p) for p in pks], _lax_signature(signature)
+        try:
+            dom8 = _dom8(domain)
+        except OverflowError:
+            if not pks:
+                dom8 = bytes(8)    # py_ecc never serialises the domain of an empty call (A.6)
+            else:
+                # the first message group's pubkeys are decoded before hash_to_G2 serialises it
+                first = min(msgs)
+                if not _pubkeys_decode([p for p, m in zip(pks, msgs) if m == first]):
+                    return False
+                raise
     with _native.subgroup_policy_scope(SUBGROUP_POLICY):
         return verify_multiple_bytes(pks, msgs, signature, dom8)
 
@@ -156,8 +240,11 @@ def use_pubkey_registry(registry) -> None:
 @only_with_bls(alt_return=STUB_PUBKEY)
 def bls_aggregate_pubkeys(pubkeys):
     pks = [bytes(p) for p in pubkeys]
-    if any(len(p) != 48 for p in pks):
-        raise ValueError("pubkeys must be 48 bytes")
+    if _strict():
+        if any(len(p) != 48 for p in pks):
+            raise ValueError("pubkeys must be 48 bytes")
+    else:
+        pks = [_lax_pubkey(p) for p in pks]
     with _native.subgroup_policy_scope(SUBGROUP_POLICY):
         if _pubkey_registry is not None:
             return _pubkey_registry.aggregate_pubkeys(pks)
@@ -167,8 +254,11 @@ def bls_aggregate_pubkeys(pubkeys):
 @only_with_bls(alt_return=STUB_SIGNATURE)
 def bls_aggregate_signatures(signatures):
     sigs = [bytes(s) for s in signatures]
-    if any(len(s) != 96 for s in sigs):
-        raise ValueError("signatures must be 96 bytes")
+    if _strict():
+        if any(len(s) != 96 for s in sigs):
+            raise ValueError("signatures must be 96 bytes")
+    else:
+        sigs = [_lax_signature(s) for s in sigs]
     with _native.subgroup_policy_scope(SUBGROUP_POLICY):
         return _native.aggregate_signatures(b"".join(sigs))
 

@@ -42,26 +42,39 @@ def build_hip(force=False, extra=(), out=None):
     deps = [os.path.join(CSRC, f) for f in HIP_SOURCES + HEADERS] + [os.path.join(INC, "bls381.h")]
     if not force and _newer(out, deps):
         return out
-    # built beside the target and renamed into place, so a snapshot of the tree taken while
-    # hipcc runs (a GPU call) sees the old library or the new one, never a partial file
-    tmp = out + ".partial"
+    import fcntl
     import shutil
     import tempfile
-    import time
-    t0 = time.time()
-    # hipcc reads the sources twice (device code, then host code, minutes apart): it compiles a
-    # snapshot, so an edit during the build can never pair one version's kernels with another's
-    # launch code (a kernel symbol the code object lacks)
-    with tempfile.TemporaryDirectory(prefix="bls381_build_") as snap:
-        shutil.copytree(CSRC, os.path.join(snap, "csrc"))
-        shutil.copytree(INC, os.path.join(snap, "include"))
-        scs = os.path.join(snap, "csrc")
-        _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I",
-              os.path.join(snap, "include"), "-I", scs, *extra, *[os.path.join(scs, f) for f in HIP_SOURCES],
-              "-o", tmp])
-    os.replace(tmp, out)
-    # stamped with the time the sources were read: a source edited during the build stays newer
-    os.utime(out, (t0, t0))
+    # one build of a target at a time (a second builder waits, then finds it current)
+    with open(out + ".lock", "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        if not force and _newer(out, deps):
+            return out
+        # built beside the target under a name of its own and renamed into place, so a snapshot of
+        # the tree taken while hipcc runs (a GPU call) sees the old library or the new one, never a
+        # partial file
+        fd, tmp = tempfile.mkstemp(prefix=os.path.basename(out) + ".", suffix=".partial", dir=os.path.dirname(out))
+        os.close(fd)
+        # the newest source mtime at the start: the library is stamped with it, so a source edited
+        # during the build stays newer (rebuilt next time) and an unchanged tree stays current
+        src_t = max(os.path.getmtime(d) for d in deps)
+        try:
+            # hipcc reads the sources twice (device code, then host code, minutes apart): it compiles
+            # a snapshot, so an edit during the build can never pair one version's kernels with
+            # another's launch code (a kernel symbol the code object lacks)
+            with tempfile.TemporaryDirectory(prefix="bls381_build_") as snap:
+                shutil.copytree(CSRC, os.path.join(snap, "csrc"))
+                shutil.copytree(INC, os.path.join(snap, "include"))
+                scs = os.path.join(snap, "csrc")
+                _run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I",
+                      os.path.join(snap, "include"), "-I", scs, *extra, *[os.path.join(scs, f) for f in HIP_SOURCES],
+                      "-o", tmp])
+            os.chmod(tmp, 0o755)
+            os.replace(tmp, out)
+        finally:
+            if os.path.exists(tmp):
+                os.unlink(tmp)
+        os.utime(out, (src_t, src_t))
     return out
 
 

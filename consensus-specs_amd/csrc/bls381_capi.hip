@@ -1355,14 +1355,17 @@ int bls381_verify_batch(size_t n, const uint8_t* pks, const uint8_t* msgs32, con
   return BLS381_EARG;
 }
 
-// Single calls run as a batch of lat_pad() identical copies (BLS381_LAT_PAD, default 32; 1 = off).
+// BLS381_LAT_PAD = k > 1 (measurement knob, default 1 = off): a single call runs as a batch of k
+// identical copies.
 // Same kernels, same per-item work and the same verdict, but measured on MI355X (r04t/r04u, one box,
 // three alternating rounds of 40 calls): bls_verify through the shim 9.95-10.06 ms median as one item,
 // 8.93-8.95 ms as 32 copies (min 8.88-8.90), 9.44-9.59 as 8, 9.05 as 128.  The per-kernel times of
 // a lone wave vary from run to run and are slower than the same wave among 32; the
-// cause is not established -- it behaves like a clock policy that reads an almost idle GPU.
+// cause is not established -- it behaves like a clock policy that reads an almost idle GPU.  The
+// padding multiplies the device work of every single call by k for any other stream or process
+// sharing the GPU, so it is opt-in.
 static int lat_pad() {
-  static const int pad = std::max(1, std::min(1024, env_knob("BLS381_LAT_PAD", 32)));
+  static const int pad = std::max(1, std::min(1024, env_knob("BLS381_LAT_PAD", 1)));
   return pad;
 }
 
@@ -2742,6 +2745,8 @@ namespace {
 constexpr size_t RB_ML_CHUNK = 32768;
 // the MSM's point lists hold 16-bit point numbers (2 per item): at most 2^15 items per sub-batch
 constexpr size_t RB_BATCH_MAX = 32768;
+// sub-batches up to this size sum their signatures with the bucket MSM (k_rb_msm_*)
+constexpr size_t RB_MSM_MAX_B = 256;
 size_t rb_slots(size_t n, size_t B) { return ((n + B - 1) / B) * (B / 2 + 1); }
 size_t rb_ml_chunk(size_t n, size_t B) { return std::min<size_t>(((n + B - 1) / B) * (B / 2), RB_ML_CHUNK); }
 size_t rb_ws_size(size_t n, size_t B) {
@@ -2826,10 +2831,14 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
     // BLS381_RB_MSM (measurement knob): 1 (default) the sub-batch sums sum_i [r_i] sig_i as one bucket
     // MSM per sub-batch (k_rb_msm_*); 0 a joint 32-bit ladder per item (k_rb_scale_g2) and a tree sum
+    // The MSM gives each (sub-batch, window, digit) bucket to one lane pair, which adds its ~B/16
+    // points in sequence: past RB_MSM_MAX_B the buckets become long dependent chains on a few lane
+    // pairs (r04e: B = 256 already equal to the ladder, 2.307 / 2.303 M/s), so larger sub-batches
+    // take the per-item ladder and the tree sum, whose work spreads over every item.
     static const int rb_msm = env_knob("BLS381_RB_MSM", 1);
     const uint32_t* sjac;
     const uint8_t* sbad;
-    if (rb_msm) {
+    if (rb_msm && B <= RB_MSM_MAX_B) {
       uint32_t* moff = b.take<uint32_t>(nb * RB_MSM_W * (RB_MSM_D + 1));
       uint16_t* midx = b.take<uint16_t>(nb * RB_MSM_W * 2 * B);
       uint32_t* mbucket = b.take<uint32_t>(6 * FP_LIMBS * nb * RB_MSM_W * RB_MSM_D);

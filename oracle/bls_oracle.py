@@ -345,10 +345,12 @@ def compress_G1(pt) -> int:
 
 def decompress_G1(z: int, strict: bool = False):
     """py_ecc 1.7.0 `decompress_G1`; strict=True: the spec's checks
-    (bls_signature.md:47-52).  Raises ValueError."""
-    if z >= 2 ** 384:
+    (bls_signature.md:47-52).  Raises ValueError.  The lax decoder reads bits 381-382 and
+    z mod 2^381 only, so any bits from 383 up (c_flag, and those of a pubkey longer than
+    48 bytes, which pubkey_to_G1 reads as one big-endian integer) are ignored."""
+    if strict and z >= 2 ** 384:
         raise ValueError("G1 encoding longer than 384 bits")
-    c_flag = z >> 383
+    c_flag = (z >> 383) & 1
     b_flag = (z >> 382) & 1
     a_flag = (z >> 381) & 1
     x = z % POW_2_381
@@ -387,12 +389,12 @@ def compress_G2(pt) -> Tuple[int, int]:
 
 def decompress_G2(p: Tuple[int, int], strict: bool = False):
     """py_ecc 1.7.0 `decompress_G2`: x = FQ2([z2, z1 mod 2^381]), both
-    reduced mod q (z2 with its top bits); strict=True: the spec's checks
+    reduced mod q (z2 with its top bits, of any length); strict=True: the spec's checks
     (bls_signature.md:58-64).  Raises ValueError."""
     z1, z2 = p
-    if z1 >= 2 ** 384 or z2 >= 2 ** 384:
+    if strict and (z1 >= 2 ** 384 or z2 >= 2 ** 384):
         raise ValueError("G2 encoding longer than 384 bits")
-    c1 = z1 >> 383
+    c1 = (z1 >> 383) & 1
     b1 = (z1 >> 382) & 1
     a1 = (z1 >> 381) & 1
     x1 = z1 % POW_2_381
@@ -435,8 +437,10 @@ def _to_bytes(b) -> bytes:
 
 
 def pubkey_to_G1(pubkey, strict: bool = False) -> tuple:
+    """py_ecc 1.7.0: decompress_G1(big_endian_to_int(pubkey)) for a pubkey of any length
+    (b"" is z = 0, the order-3 point (0, 2)); strict: the spec's Bytes48 only."""
     pubkey = _to_bytes(pubkey)
-    if len(pubkey) != 48:
+    if strict and len(pubkey) != 48:
         raise ValueError("pubkey must be 48 bytes")
     return decompress_G1(int.from_bytes(pubkey, "big"), strict)
 
@@ -446,8 +450,10 @@ def G1_to_pubkey(pt) -> bytes:
 
 
 def signature_to_G2(signature, strict: bool = False) -> tuple:
+    """py_ecc 1.7.0: decompress_G2((big_endian_to_int(signature[:48]),
+    big_endian_to_int(signature[48:]))) for a signature of any length; strict: Bytes96 only."""
     signature = _to_bytes(signature)
-    if len(signature) != 96:
+    if strict and len(signature) != 96:
         raise ValueError("signature must be 96 bytes")
     return decompress_G2((int.from_bytes(signature[:48], "big"),
                           int.from_bytes(signature[48:], "big")), strict)
@@ -675,6 +681,10 @@ def verify_multiple(pubkeys: Sequence[bytes], message_hashes: Sequence[bytes],
     try:
         o = FQ12_ONE
         msgs = [bytes(m) for m in message_hashes]
+        # py_ecc iterates set(message_hashes), whose order is Python's hash order; the
+        # product is the same in any order, and only what comes first when a decode fails
+        # or the domain is out of range (its groups' pubkeys are decoded before hash_to_G2
+        # serialises the domain) depends on it: sorted order here and in the shim
         for m_pubs in sorted(set(msgs)):
             group_pub = Z1
             for i in range(len_msgs):
@@ -716,7 +726,11 @@ def in_G2(pt) -> bool:
     return pt_is_inf(_Fq2Ops, pt_multiply(_Fq2Ops, pt, r))
 
 
+# The spec types domain as uint64 (bls_signature.md:131,139), so under this policy an
+# out-of-range domain raises OverflowError before anything is decoded; py_ecc (verify,
+# verify_multiple above) serialises it inside hash_to_G2, after the decodes before it.
 def verify_strict(message_hash: bytes, pubkey: bytes, signature: bytes, domain: int) -> bool:
+    domain_to_bytes8(domain)
     try:
         if not in_G1(pubkey_to_G1(pubkey, True)) or not in_G2(signature_to_G2(signature, True)):
             return False
@@ -730,6 +744,7 @@ def verify_multiple_strict(pubkeys: Sequence[bytes], message_hashes: Sequence[by
     if len(pubkeys) != len(message_hashes):
         raise ValidationError(
             "len(pubkeys) (%s) should be equal to len(message_hashes) (%s)" % (len(pubkeys), len(message_hashes)))
+    domain_to_bytes8(domain)
     try:
         if not all(in_G1(pubkey_to_G1(p, True)) for p in pubkeys) or not in_G2(signature_to_G2(signature, True)):
             return False

@@ -69,14 +69,24 @@ def test_errors_raised_before_the_engine():
         bls.bls_verify_multiple([b"\x00" * 48], [], b"\x00" * 96, 0)
     with pytest.raises(bls.ValidationError):
         bls.bls_verify_multiple([], [b"\x00" * 32], b"\x00" * 96, 0)
-    with pytest.raises(OverflowError):
-        bls.bls_verify(b"\x00" * 48, b"\x00" * 32, b"\x00" * 96, 2 ** 64)
-    with pytest.raises(OverflowError):
-        bls.bls_verify(b"\x00" * 48, b"\x00" * 32, b"\x00" * 96, -1)
-    # wrong-length encodings are invalid inputs -> False without reaching the device
-    assert bls.bls_verify(b"\x00" * 47, b"\x00" * 32, b"\x00" * 96, 0) is False
-    with pytest.raises(ValueError):
-        bls.bls_aggregate_pubkeys([b"\x00" * 47])
+    # the strict policy takes the spec's types: a uint64 domain, checked first, and Bytes48 /
+    # Bytes96 (other lengths are invalid inputs -> False without reaching the device).  Under
+    # the py_ecc policy both need the engine (py_ecc decodes before it serialises the domain,
+    # and reads other lengths as integers): tests/test_gpu_parity.py::test_shim_lengths_and_domain_order
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = "strict"
+    try:
+        with pytest.raises(OverflowError):
+            bls.bls_verify(b"\x00" * 48, b"\x00" * 32, b"\x00" * 96, 2 ** 64)
+        with pytest.raises(OverflowError):
+            bls.bls_verify(b"\x00" * 48, b"\x00" * 32, b"\x00" * 96, -1)
+        with pytest.raises(OverflowError):
+            bls.bls_verify_multiple([], [], b"\x00" * 96, 2 ** 64)
+        assert bls.bls_verify(b"\x00" * 47, b"\x00" * 32, b"\x00" * 96, 0) is False
+        with pytest.raises(ValueError):
+            bls.bls_aggregate_pubkeys([b"\x00" * 47])
+    finally:
+        bls.SUBGROUP_POLICY = old
 
 
 def test_keyword_names_match_reference():
@@ -141,14 +151,16 @@ def test_thread_policy_override_is_per_thread():
 
 def test_shim_does_not_rewrite_process_policy():
     """bls.bls_verify scopes its policy to the call: a process-wide 'strict' set by another
-    front end survives a shim call (here one that stops before the device: a wrong length)."""
+    front end survives a shim call (here one that stops before the device: a wrong length
+    under the shim's strict policy, while the process-wide policy is py_ecc's)."""
     from bls381_amd import _native, bls
-    _native.set_subgroup_policy("strict")
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = "strict"
     try:
         assert bls.bls_verify(b"\x00" * 47, b"\x00" * 32, b"\x00" * 96, 0) is False
-        assert _native.get_subgroup_policy() == "strict"
+        assert _native.get_subgroup_policy() == "pyecc"
     finally:
-        _native.set_subgroup_policy("pyecc")
+        bls.SUBGROUP_POLICY = old
 
 
 def test_rccl_path_resolves_without_a_device():

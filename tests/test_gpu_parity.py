@@ -1204,6 +1204,50 @@ def test_randomized_batch_clean_and_tampered(native, n):
         assert np.array_equal(v, want) and st[2] > 0 and st[0] + st[1] == n, B
 
 
+def test_randomized_batch_largest_sub_batches(native):
+    """The largest sub-batches: B = 32,768, the 16-bit point-number limit of the MSM
+    lists, which now takes the per-item ladder and the tree sum, and B = 256, the largest MSM
+    sub-batch, over 2^16 + 3 items (a ragged 3-item last sub-batch).  Clean: every sub-batch
+    passes; one tampered item in the first sub-batch: exactly that sub-batch fails and its
+    items are re-verified to the default path's verdicts."""
+    import ctypes
+    import os as _os
+    import torch
+    L = native.lib()
+    n = (1 << 16) + 3
+    rng = np.random.default_rng(23)
+    sk = 0xBA7C4
+    pk = O.privtopub(sk)
+    ms = [bytes(rng.integers(0, 256, 32, dtype=np.uint8)) for _ in range(32)]
+    ss = native.sign_batch(b"".join(ms), sk.to_bytes(32, "big") * 32, (3).to_bytes(8, "big") * 32)
+    idx = rng.integers(0, 32, n)
+    msgs = b"".join(ms[i] for i in idx)
+    sigs = bytearray(b"".join(ss[96 * i:96 * i + 96] for i in idx))
+    doms = (3).to_bytes(8, "big") * n
+    dev = torch.device("cuda", 0)
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def run(sig_bytes, B):
+        d = [t(pk * n), t(msgs), t(bytes(sig_bytes)), t(doms)]
+        v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        ws = torch.empty(L.bls381_verify_batch_randomized_workspace_size(n, B), dtype=torch.uint8, device=dev)
+        st = (ctypes.c_uint64 * 3)()
+        native.check(L.bls381_verify_batch_randomized_device(n, *[x.data_ptr() for x in d], _os.urandom(32), B,
+                                                             v.data_ptr(), ws.data_ptr(),
+                                                             ctypes.c_void_p(stream.cuda_stream), st))
+        return v.cpu().numpy().astype(bool), list(st)
+
+    for B in (32768, 256):
+        v, st = run(sigs, B)
+        assert v.all() and st == [n, 0, 0], B
+    j = next(k for k in range(1, 32) if idx[k] != idx[0])
+    sigs[0:96] = sigs[96 * j:96 * j + 96]
+    for B in (32768, 256):
+        v, st = run(sigs, B)
+        assert not v[0] and v[1:].all() and st[2] == 1 and st[1] == B, (B, st)
+
+
 # ---------------------------- octet-layout final exponentiation (latency knob)
 _OCT_SCRIPT = r"""
 import json, os, sys
@@ -1246,3 +1290,125 @@ def test_octet_final_exponentiation_knob():
     r = subprocess.run([sys.executable, "-c", _OCT_SCRIPT, root], env=env, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0 and "octet fe ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+# ------------------------------- full-size C3 epoch
+def test_c3_full_epoch_three_forms_agree(native):
+    """The mainnet-preset epoch at full size: 1,024 committees x 128 members drawn from 8,192
+    validators (privkeys 1..8192, helpers/keys.py's small-integer keys), each attestation checked
+    the way validate_indexed_attestation does it (0_beacon-chain.md:1023-1034):
+    bls_aggregate_pubkeys(committee), bls_aggregate_pubkeys([]) (custody bit 1 is always empty in
+    phase 0) and bls_verify_multiple([agg, agg_inf], [m0, m1], sig, DOMAIN_ATTESTATION), with
+    1/16 of the attestations signed over a different m0.  The two-call form (aggregates left in
+    HBM, then the verify batch), the grouped call and the grouped call over a registry must agree
+    call by call with the construction; the oracle re-derives the aggregates and the verdicts of
+    four attestations: a valid one, a tampered one, and the infinity aggregate of the empty group."""
+    import ctypes
+    import torch
+    from bls381_amd.registry import PubkeyRegistry
+    L = native.lib()
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream(dev)
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    nv, nc, cs = 8192, 1024, 128
+    sk = list(range(1, nv + 1))
+    pks = native.privtopub_batch(b"".join(k.to_bytes(32, "big") for k in sk))
+    rng = np.random.default_rng(0xB15_0003)
+    idx = np.stack([rng.choice(nv, cs, replace=False) for _ in range(nc)]).reshape(-1)
+    pk_arr = np.frombuffer(pks, dtype=np.uint8).reshape(nv, 48)
+    offsets = np.repeat(np.arange(0, nc * cs + 1, cs, dtype=np.uint32), 2)[1:]   # groups 2c, 2c+1 (empty)
+    m0 = bytearray(rng.bytes(32 * nc))
+    m1 = rng.bytes(32 * nc)
+    ssum = [int(sum(sk[j] for j in idx[c * cs:(c + 1) * cs])) % O.r for c in range(nc)]
+    sigs = native.sign_batch(bytes(m0), b"".join(k.to_bytes(32, "big") for k in ssum), (2).to_bytes(8, "big") * nc)
+    expected = np.ones(nc, dtype=bool)
+    for c in range(5, nc, 16):
+        m0[32 * c + 7] ^= 0x80
+        expected[c] = False
+    msgs = b"".join(bytes(m0[32 * c:32 * c + 32]) + m1[32 * c:32 * c + 32] for c in range(nc))
+    call_off = np.arange(0, 2 * nc + 1, 2, dtype=np.uint32)
+    doms = (2).to_bytes(8, "big") * nc
+    d_cpks, d_sigs, d_doms = t(pk_arr[idx].tobytes()), t(sigs), t(doms)
+    cvp = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    # two calls: aggregates in HBM, then the verify_multiple batch over them
+    d_out = torch.zeros(2 * nc * 48, dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(2 * nc, dtype=torch.int32, device=dev)
+    aws = torch.empty(L.bls381_aggregate_pubkeys_batch_workspace_size(2 * nc, nc * cs), dtype=torch.uint8, device=dev)
+    native.check(L.bls381_aggregate_pubkeys_batch_device(2 * nc, cvp(offsets), nc * cs, d_cpks.data_ptr(),
+                                                         d_out.data_ptr(), d_st.data_ptr(), aws.data_ptr(), sp))
+    d_v1 = torch.zeros(nc, dtype=torch.uint8, device=dev)
+    vws = torch.empty(L.bls381_verify_multiple_batch_workspace_size(nc, 2 * nc, 32), dtype=torch.uint8, device=dev)
+    native.check(L.bls381_verify_multiple_batch_device(nc, cvp(call_off), msgs, 32, d_out.data_ptr(), d_sigs.data_ptr(),
+                                                       d_doms.data_ptr(), d_v1.data_ptr(), vws.data_ptr(), sp))
+    # one grouped call, and the same over a registry of the 8,192 keys
+    gws = torch.empty(L.bls381_verify_multiple_grouped_workspace_size(nc, 2 * nc, nc * cs, 32), dtype=torch.uint8,
+                      device=dev)
+    d_v2 = torch.zeros(nc, dtype=torch.uint8, device=dev)
+    native.check(L.bls381_verify_multiple_grouped_device(nc, cvp(call_off), 2 * nc, cvp(offsets), msgs, 32,
+                                                         d_cpks.data_ptr(), d_sigs.data_ptr(), d_doms.data_ptr(),
+                                                         d_v2.data_ptr(), gws.data_ptr(), sp))
+    reg = PubkeyRegistry(nv)
+    try:
+        ent = reg.add([pks[48 * i:48 * i + 48] for i in range(nv)])
+        assert np.all(ent >= 0)
+        d_ent = t(ent[idx].astype(np.uint32).tobytes())
+        d_v3 = torch.zeros(nc, dtype=torch.uint8, device=dev)
+        native.check(L.bls381_registry_verify_multiple_grouped_device(
+            reg._h, nc, cvp(call_off), 2 * nc, cvp(offsets), msgs, 32, d_ent.data_ptr(), d_sigs.data_ptr(),
+            d_doms.data_ptr(), d_v3.data_ptr(), gws.data_ptr(), sp))
+        torch.cuda.synchronize()
+        v3 = d_v3.cpu().numpy().astype(bool)
+    finally:
+        reg.close()
+    torch.cuda.synchronize()
+    assert int(d_st.abs().sum().item()) == 0
+    v1, v2 = d_v1.cpu().numpy().astype(bool), d_v2.cpu().numpy().astype(bool)
+    assert np.array_equal(v1, expected) and np.array_equal(v2, expected) and np.array_equal(v3, expected)
+    aggs = d_out.cpu().numpy().tobytes()
+    inf = bytes([0xC0]) + bytes(47)
+    for c in (0, 5, 21, 1023):            # valid, tampered (c % 16 == 5), tampered, valid
+        agg, agg1 = aggs[96 * c:96 * c + 48], aggs[96 * c + 48:96 * c + 96]
+        members = [pks[48 * j:48 * j + 48] for j in idx[c * cs:(c + 1) * cs]]
+        assert agg == O.aggregate_pubkeys(members) and agg1 == O.aggregate_pubkeys([]) == inf, c
+        want = O.verify_multiple([agg, agg1], [msgs[64 * c:64 * c + 32], msgs[64 * c + 32:64 * c + 64]],
+                                 sigs[96 * c:96 * c + 96], 2)
+        assert want == bool(expected[c]), c
+
+
+# ------------------------------ the boundary's residual py_ecc behaviours (VERDICT r04 #4, #7)
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_shim_lengths_and_domain_order(native, noncanon, policy):
+    """bls_noncanonical.json shim_* cases through the bls shim under each policy: pubkeys and
+    signatures of other lengths (py_ecc reads them as integers; strict: Bytes48 / Bytes96), and
+    an out-of-range domain, which py_ecc serialises after the decodes preceding hash_to_G2."""
+    from bls381_amd import bls
+    col, ocol = "expected_" + policy, "output_" + policy
+
+    def outcome(fn, *a):
+        try:
+            return fn(*a)
+        except (OverflowError, bls.ValidationError) as e:
+            return type(e).__name__
+
+    old = bls.SUBGROUP_POLICY
+    bls.SUBGROUP_POLICY = policy
+    try:
+        for c in noncanon["shim_verify"]:
+            got = outcome(bls.bls_verify, bytes.fromhex(c["pubkey"]), bytes.fromhex(c["message"]),
+                          bytes.fromhex(c["signature"]), int(c["domain"]))
+            assert got == c[col], (c["kind"], got)
+        for c in noncanon["shim_verify_multiple"]:
+            got = outcome(bls.bls_verify_multiple, [bytes.fromhex(p) for p in c["pubkeys"]],
+                          [bytes.fromhex(m) for m in c["messages"]], bytes.fromhex(c["signature"]), int(c["domain"]))
+            assert got == c[col], (c["kind"], got)
+        for name, fn in (("shim_aggregate_pubkeys", bls.bls_aggregate_pubkeys),
+                         ("shim_aggregate_sigs", bls.bls_aggregate_signatures)):
+            for c in noncanon[name]:
+                try:
+                    got = fn([bytes.fromhex(x) for x in c["input"]]).hex()
+                except ValueError:
+                    got = None
+                assert got == c[ocol], (name, c["kind"])
+    finally:
+        bls.SUBGROUP_POLICY = old

@@ -100,3 +100,28 @@ def test_golden_batch_verdicts_sample(golden):
     for it in gb["verify"][:2] + gb["verify"][16:18] + gb["verify"][-6:]:
         assert O.verify(bytes.fromhex(it["message"]), bytes.fromhex(it["pubkey"]),
                         bytes.fromhex(it["signature"]), int(it["domain"])) == it["expected"], it["kind"]
+
+
+def test_oracle_matches_spec_text():
+    """The oracle's hash_to_G2 and modular_squareroot against the reference's own text:
+    tests/golden/spec_text_hash.json holds the outputs of the ```python blocks of
+    specs/bls_signature.md:68-108, run unmodified by tests/golden/make_spec_text_vectors.py
+    (pulled with the reference's scripts/function_puller.py fence rule).  The text leaves
+    bytes8's byte order open; the big-endian column is the oracle's DOMAIN_BYTEORDER (SURVEY
+    A.2), and the little-endian column differs exactly where a domain is not a palindrome."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "spec_text_hash.json")) as f:
+        st = json.load(f)
+    assert O.DOMAIN_BYTEORDER == "big"
+    for c in st["hash_to_G2"]:
+        m, d = bytes.fromhex(c["message"]), int(c["domain"])
+        (xr, xi), (yr, yi) = O.g2_affine(O.hash_to_G2(m, d))
+        assert [hex(xr), hex(xi), hex(yr), hex(yi)] == c["affine_big"], (c["message"][:8], d)
+        same = d.to_bytes(8, "big") == d.to_bytes(8, "little")
+        assert (c["affine_little"] == c["affine_big"]) == same, d
+    for c in st["modular_squareroot"]:
+        v = (int(c["input"][0], 16), int(c["input"][1], 16))
+        r = O.modular_squareroot(v)
+        assert (None if r is None else [hex(r[0]), hex(r[1])]) == c["output"]
+    assert len(st["hash_to_G2"]) >= 15 and any(c["output"] is None for c in st["modular_squareroot"])

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests/ -x -v -m gpu -p no:cacheprovider --
  && echo "tests ok" && tail -1 gpurun_out/gpu_tests_$TAG.log \
  && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 \
  && echo "smoke ok" \
- && timeout -k 10 900 python bench.py --steps 5 --warmup 1 > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
+ && timeout -k 10 900 python bench.py --steps 5 --warmup 1 --fail-on-secondary-error > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err \
  && echo "bench ok" \
  && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o prof -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-secondary --no-aggregate > gpurun_out/rocprof_$TAG.log 2>&1 \
  && echo "rocprof ok" \
