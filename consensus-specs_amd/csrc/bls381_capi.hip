@@ -2337,12 +2337,12 @@ __global__ void __launch_bounds__(KBLOCK) k_fp12_row(const uint32_t* __restrict_
   const int p = pr_odd() ? 1 : 0;
   const bool ok = st[0] == ST_OK;
   const fp12p_t a = soa_ld12(f, 1, 0);
-  const fp2p_t* cs[6] = {&a.c0.c0, &a.c0.c1, &a.c0.c2, &a.c1.c0, &a.c1.c1, &a.c1.c2};
-  for (int k = 0; k < 6; ++k) {
+  auto put = [&](int k, const fp2p_t& c) {
     uint8_t* o = out576 + 96 * k + 48 * p;
-    if (ok) fp_plain_to_be48(o, fp_from_mont(cs[k]->v));
+    if (ok) fp_plain_to_be48(o, fp_from_mont(c.v));
     else for (int b = 0; b < 48; ++b) o[b] = 0;
-  }
+  };
+  put(0, a.c0.c0); put(1, a.c0.c1); put(2, a.c0.c2); put(3, a.c1.c0); put(4, a.c1.c1); put(5, a.c1.c2);
 }
 
 // compressed partial aggregate, or 48 zero bytes (not a valid encoding) when its status is an error

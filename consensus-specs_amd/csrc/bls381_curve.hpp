@@ -58,7 +58,7 @@ BLS_INLINE jac_t<F> jac_neg(const jac_t<F>& p) { jac_t<F> r = p; r.y = f_neg(p.y
 
 // dbl-2009-l (a = 0): 2M + 5S
 template <class F>
-BLS_HD inline jac_t<F> jac_dbl(const jac_t<F>& p) {
+BLS_DEV_INLINE jac_t<F> jac_dbl(const jac_t<F>& p) {
   const F A = f_sqr(p.x);
   const F B = f_sqr(p.y);
   const F C = f_sqr(B);
@@ -75,7 +75,7 @@ BLS_HD inline jac_t<F> jac_dbl(const jac_t<F>& p) {
 
 // add-2007-bl full Jacobian addition with the exceptional cases
 template <class F>
-BLS_HD inline jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
+BLS_DEV_INLINE jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
   if (jac_is_inf(p)) return q;
   if (jac_is_inf(q)) return p;
   const F Z1Z1 = f_sqr(p.z);
@@ -102,7 +102,7 @@ BLS_HD inline jac_t<F> jac_add(const jac_t<F>& p, const jac_t<F>& q) {
 
 // mixed addition p + (x2, y2) with an affine, finite second operand
 template <class F>
-BLS_HD inline jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
+BLS_DEV_INLINE jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
   if (jac_is_inf(p)) return jac_from_aff(q);
   const F Z1Z1 = f_sqr(p.z);
   const F U2 = f_mul(q.x, Z1Z1);
@@ -124,7 +124,7 @@ BLS_HD inline jac_t<F> jac_add_aff(const jac_t<F>& p, const aff_t<F>& q) {
 }
 
 template <class F>
-BLS_HD inline bool jac_to_aff(aff_t<F>& out, const jac_t<F>& p) {
+BLS_DEV_INLINE bool jac_to_aff(aff_t<F>& out, const jac_t<F>& p) {
   if (jac_is_inf(p)) return false;
   const F zi = f_inv(p.z);
   const F zi2 = f_sqr(zi);
@@ -137,7 +137,7 @@ BLS_HD inline bool jac_to_aff(aff_t<F>& out, const jac_t<F>& p) {
 // formulas inlined into the loop, so the running point stays in registers.
 // [k] a for a 64-bit scalar, affine base, left-to-right
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
+BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F> a, uint64_t k) {
   jac_t<F> r = jac_from_aff(a);
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -152,7 +152,7 @@ BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F>& a, uint64_t k) {
 // with s = endo(a) for an endomorphism acting as [mu] this is [k0 + mu k1] a at half the
 // doublings of a 64-bit multiplication (the randomized-batch weights)
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_2x32(const aff_t<F>& a, const aff_t<F>& s, uint32_t k0, uint32_t k1) {
+BLS_NOINLINE jac_t<F> jac_mul_2x32(const aff_t<F> a, const aff_t<F> s, uint32_t k0, uint32_t k1) {
   jac_t<F> r = jac_infinity<F>();
   const uint32_t any = k0 | k1;
   int top = 31;
@@ -167,7 +167,7 @@ BLS_NOINLINE jac_t<F> jac_mul_2x32(const aff_t<F>& a, const aff_t<F>& s, uint32_
 
 // [k] p for a 64-bit scalar, Jacobian base
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {
+BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F> p, uint64_t k) {
   jac_t<F> r = p;
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -178,13 +178,17 @@ BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F>& p, uint64_t k) {
   return r;
 }
 
-// [k] a for a little-endian multi-limb scalar (nbits significant bits)
+// a scalar of up to 512 bits, little-endian 32-bit words, passed by value (no pointer into the
+// caller's private memory crosses a call: DESIGN.md §10.8)
+struct scalar_t { uint32_t w[16]; };
+
+// [k] a for a little-endian multi-limb scalar (nbits <= 512 significant bits)
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_limbs(const aff_t<F>& a, const uint32_t* k, int nbits) {
+BLS_NOINLINE jac_t<F> jac_mul_limbs(const aff_t<F> a, const scalar_t k, int nbits) {
   jac_t<F> r = jac_infinity<F>();
   for (int i = nbits - 1; i >= 0; --i) {
     r = jac_dbl(r);
-    if ((k[i >> 5] >> (i & 31)) & 1u) r = jac_add_aff(r, a);
+    if ((k.w[i >> 5] >> (i & 31)) & 1u) r = jac_add_aff(r, a);
   }
   return r;
 }
@@ -202,7 +206,7 @@ enum : int { PT_OK = 0, PT_INF = 1, PT_BAD = 2 };
 //     mod q; c_flag and x < q are never looked at.
 // Both accept every canonical encoding with the same point; the lax decoder also
 // accepts non-canonical encodings (strict PT_BAD).  g1_canonical tells them apart.
-BLS_HD inline bool g1_canonical(const uint8_t* b48) {
+BLS_DEV_INLINE bool g1_canonical(const uint8_t* b48) {
   const uint8_t top = b48[0];
   const int c_flag = (top >> 7) & 1, b_flag = (top >> 6) & 1, a_flag = (top >> 5) & 1;
   uint8_t tmp[48];
@@ -215,7 +219,7 @@ BLS_HD inline bool g1_canonical(const uint8_t* b48) {
 }
 
 // G1 decompress (bls_signature.md:36-52 / py_ecc decompress_G1).  PT_OK / PT_INF / PT_BAD.
-BLS_HD inline int g1_decompress(aff_t<fp_t>& out, const uint8_t* b48, bool lax) {
+BLS_DEV_INLINE int g1_decompress(aff_t<fp_t>& out, const uint8_t* b48, bool lax) {
   const uint8_t top = b48[0];
   const int b_flag = (top >> 6) & 1, a_flag = (top >> 5) & 1;
   if (!lax && !g1_canonical(b48)) return PT_BAD;
@@ -234,7 +238,7 @@ BLS_HD inline int g1_decompress(aff_t<fp_t>& out, const uint8_t* b48, bool lax) 
   return PT_OK;
 }
 
-BLS_HD inline void g1_compress(uint8_t* b48, const jac_t<fp_t>& p) {
+BLS_DEV_INLINE void g1_compress(uint8_t* b48, const jac_t<fp_t>& p) {
   aff_t<fp_t> a;
   if (!jac_to_aff(a, p)) {
     for (int i = 0; i < 48; ++i) b48[i] = 0;
@@ -255,7 +259,7 @@ BLS_INLINE int g2_y_flag(const fp2_t& y_mont) {
 }
 
 // strict-codec acceptance of a G2 encoding (bls_signature.md:58-64)
-BLS_HD inline bool g2_canonical(const uint8_t* b96) {
+BLS_DEV_INLINE bool g2_canonical(const uint8_t* b96) {
   const uint8_t top = b96[0];
   const int c1 = (top >> 7) & 1, b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
   if (b96[48] & 0xe0) return false;               // a_flag2 == b_flag2 == c_flag2 == 0
@@ -271,7 +275,7 @@ BLS_HD inline bool g2_canonical(const uint8_t* b96) {
 
 // G2 decompress (bls_signature.md:54-64 / py_ecc decompress_G2): z1 = flags | x_im,
 // z2 = x_re (lax: all 384 bits of z2, flags included, reduced mod q)
-BLS_HD inline int g2_decompress(aff_t<fp2_t>& out, const uint8_t* b96, bool lax) {
+BLS_DEV_INLINE int g2_decompress(aff_t<fp2_t>& out, const uint8_t* b96, bool lax) {
   const uint8_t top = b96[0];
   const int b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
   if (!lax && !g2_canonical(b96)) return PT_BAD;
@@ -293,13 +297,13 @@ BLS_HD inline int g2_decompress(aff_t<fp2_t>& out, const uint8_t* b96, bool lax)
   return PT_OK;
 }
 
-BLS_HD inline void g2_compress_aff(uint8_t* b96, const aff_t<fp2_t>& a) {
+BLS_DEV_INLINE void g2_compress_aff(uint8_t* b96, const aff_t<fp2_t>& a) {
   fp_plain_to_be48(b96, fp_from_mont(a.x.c1));
   fp_plain_to_be48(b96 + 48, fp_from_mont(a.x.c0));
   b96[0] |= 0x80 | (g2_y_flag(a.y) ? 0x20 : 0);
 }
 
-BLS_HD inline void g2_compress(uint8_t* b96, const jac_t<fp2_t>& p) {
+BLS_DEV_INLINE void g2_compress(uint8_t* b96, const jac_t<fp2_t>& p) {
   aff_t<fp2_t> a;
   if (!jac_to_aff(a, p)) {
     for (int i = 0; i < 96; ++i) b96[i] = 0;
@@ -311,7 +315,7 @@ BLS_HD inline void g2_compress(uint8_t* b96, const jac_t<fp2_t>& p) {
 
 // ---------------------------------------------------- subgroup checks -----
 // G1: sigma(P) = (beta x, y) acts on G1 as [-x^2]; P in G1 iff sigma(P) == -[x^2]P.
-BLS_HD inline bool g1_in_subgroup(const aff_t<fp_t>& p) {
+BLS_DEV_INLINE bool g1_in_subgroup(const aff_t<fp_t>& p) {
   const jac_t<fp_t> t = jac_mul_u64_jac(jac_mul_u64(p, BLS_X_ABS), BLS_X_ABS);  // [x^2] P
   if (jac_is_inf(t)) return false;
   const fp_t zz = fp_sqr(t.z);
@@ -331,7 +335,7 @@ BLS_INLINE aff_t<E> g2_psi(const aff_t<E>& a) {
 
 // G2: Q in G2 iff psi(Q) == [x]Q = -[|x|]Q
 template <class E>
-BLS_HD inline bool g2_in_subgroup(const aff_t<E>& q) {
+BLS_DEV_INLINE bool g2_in_subgroup(const aff_t<E>& q) {
   const jac_t<E> t = jac_mul_u64(q, BLS_X_ABS);
   if (jac_is_inf(t)) return false;
   const aff_t<E> s = g2_psi(q);

@@ -17,6 +17,10 @@
 #define BLS_HD __host__ __device__
 #define BLS_INLINE __host__ __device__ __forceinline__
 #define BLS_NOINLINE __host__ __device__ __attribute__((noinline))
+// always inlined on the device (a non-inlined function taking references or
+// pointers into its caller's private memory makes flat accesses to the private aperture);
+// an ordinary inline function in the host unit-test build, which keeps g++ fast
+#define BLS_DEV_INLINE __host__ __device__ __forceinline__
 #define BLS_CONST __device__ __constant__ static constexpr
 #else
 #define BLS_PHASE() ((void)0)
@@ -24,6 +28,7 @@
 #define BLS_HD
 #define BLS_INLINE inline __attribute__((always_inline))
 #define BLS_NOINLINE __attribute__((noinline))
+#define BLS_DEV_INLINE inline
 #define BLS_CONST static constexpr
 #endif
 

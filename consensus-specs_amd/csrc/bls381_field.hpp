@@ -320,7 +320,7 @@ BLS_INLINE fp_t fp_mul_small(const fp_t& a, int k) {
 }
 
 // left-to-right square-and-multiply over a 12-word little-endian (u32) exponent
-BLS_HD inline fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
+BLS_DEV_INLINE fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
   fp_t r = FP_ONE_M;
   for (int i = nbits - 1; i >= 0; --i) {
     r = fp_sqr(r);
@@ -333,7 +333,7 @@ BLS_HD inline fp_t fp_pow_limbs(const fp_t& a, const uint32_t* e, int nbits) {
 // (375 squarings + 78 multiplications + 8 for the odd-power table, against 605
 // for plain square-and-multiply).  Every square root and inversion is built
 // from this one power: sqrt(a) = u a, 1/a = u^4 a, 1/sqrt(a) = u^3 a.
-BLS_HD inline fp_t fp_pow_qm3d4(const fp_t& a) {
+BLS_HD inline fp_t fp_pow_qm3d4(const fp_t a) {
   const fp_t a2 = fp_sqr(a);
   const fp_t t1 = a, t3 = fp_mul(t1, a2), t5 = fp_mul(t3, a2), t7 = fp_mul(t5, a2);
   const fp_t t9 = fp_mul(t7, a2), t11 = fp_mul(t9, a2), t13 = fp_mul(t11, a2), t15 = fp_mul(t13, a2);
@@ -356,10 +356,10 @@ BLS_HD inline fp_t fp_pow_qm3d4(const fp_t& a) {
 }
 
 // (fp_inv: optimized binary GCD, below the word helpers)
-BLS_HD inline fp_t fp_inv(const fp_t& a);
+BLS_HD inline fp_t fp_inv(const fp_t am);
 
 // returns true and sets r when a is a square; r = a^((q+1)/4)
-BLS_HD inline bool fp_sqrt(fp_t& r, const fp_t& a) {
+BLS_DEV_INLINE bool fp_sqrt(fp_t& r, const fp_t& a) {
   r = fp_mul(fp_pow_qm3d4(a), a);
   return fp_eq(fp_sqr(r), a);
 }
@@ -499,7 +499,7 @@ BLS_INLINE uint32_t words_strip_twos(uint32_t a[12]) {
 // funnel shift): about 270 steps of ~80 word ops, an order of magnitude below
 // Euler's criterion a^((q-1)/2), so the try-and-increment loop of hash_to_G2
 // pays a full square root only for the candidate that succeeds.
-BLS_HD inline int fp_legendre(const fp_t& am) {
+BLS_HD inline int fp_legendre(const fp_t am) {
   uint32_t a[12], n[12];
   fp_plain_to_words(a, fp_from_mont(am));
   fp_plain_to_words(n, FP_Q_PLAIN);
@@ -610,7 +610,7 @@ BLS_INLINE fp_t fp_from_words(const uint32_t w[12]) {
 // of ~150 word ops, the slowest lane of a wave setting the count), then
 // A^-1 R^3 R^-1 = a^-1 R by one Montgomery product.  The safety net of fp_inv.
 // Invariants: x1 A = u, x2 A = v (mod q); u, v odd after each strip; x1, x2 < 2q.
-BLS_HD inline fp_t fp_inv_xgcd(const fp_t& am) {
+BLS_HD inline fp_t fp_inv_xgcd(const fp_t am) {
   uint32_t u[12], v[12], x1[12], x2[12];
   fp_plain_to_words(u, fp_reduce_once(am));
   uint32_t z = 0;
@@ -739,7 +739,7 @@ BLS_INLINE void inv_neg(int32_t x[INV_L]) {
   }
 }
 
-BLS_HD inline fp_t fp_inv(const fp_t& am) {
+BLS_HD inline fp_t fp_inv(const fp_t am) {
   uint32_t w[12];
   fp_plain_to_words(w, fp_reduce_once(am));
   uint32_t z = 0;
@@ -941,7 +941,7 @@ BLS_INLINE fp2_t fp2_3p2(const fp2_t& X, const fp2_t& x) {
   fp2_t r; r.c0 = fp_3p2(X.c0, x.c0); r.c1 = fp_3p2(X.c1, x.c1); return r;
 }
 
-BLS_HD inline fp2_t fp2_inv(const fp2_t& a) {
+BLS_HD inline fp2_t fp2_inv(const fp2_t a) {
   const fp_t n = fp_add(fp_sqr(a.c0), fp_sqr(a.c1));
   const fp_t ni = fp_inv(n);
   fp2_t r;
@@ -953,7 +953,7 @@ BLS_HD inline fp2_t fp2_inv(const fp2_t& a) {
 // Complex-method square root for q = 3 mod 4 (DESIGN.md "Square roots").
 // Returns false when a is a non-square.  Which of the two roots is returned
 // is unspecified; callers apply the spec's selection rule.
-BLS_HD inline bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
+BLS_DEV_INLINE bool fp2_sqrt(fp2_t& r, const fp2_t& a) {
   if (fp_is_zero(a.c1)) {
     fp_t s;
     if (fp_sqrt(s, a.c0)) { r.c0 = s; r.c1 = fp_zero(); return true; }
@@ -1008,7 +1008,7 @@ BLS_INLINE fp6_g<E> fp6_mul_inl(const fp6_g<E>& a, const fp6_g<E>& b) {
 }
 
 template <class E>
-BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E>& a, const fp6_g<E>& b) { return fp6_mul_inl(a, b); }
+BLS_NOINLINE fp6_g<E> fp6_mul(const fp6_g<E> a, const fp6_g<E> b) { return fp6_mul_inl(a, b); }
 
 template <class E>
 BLS_INLINE fp6_g<E> fp6_mul_by_v(const fp6_g<E>& a) {
@@ -1030,7 +1030,7 @@ BLS_INLINE fp6_g<E> fp6_dbl(const fp6_g<E>& a) {
 }
 
 template <class E>
-BLS_HD inline fp6_g<E> fp6_inv(const fp6_g<E>& a) {
+BLS_HD inline fp6_g<E> fp6_inv(const fp6_g<E> a) {
   const E c0 = fp2_sub(fp2_sqr(a.c0), fp2_mul_xi(fp2_mul(a.c1, a.c2)));
   const E c1 = fp2_sub(fp2_mul_xi(fp2_sqr(a.c2)), fp2_mul(a.c0, a.c1));
   const E c2 = fp2_sub(fp2_sqr(a.c1), fp2_mul(a.c0, a.c2));
@@ -1070,7 +1070,7 @@ BLS_INLINE fp12_g<E> fp12_mul_inl(const fp12_g<E>& a, const fp12_g<E>& b) {
 // call version (loops of products, e.g. the segmented Fp12 products): its 84-word
 // operands go through the stack, so the final exponentiation inlines instead
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E>& a, const fp12_g<E>& b) {
+BLS_NOINLINE fp12_g<E> fp12_mul(const fp12_g<E> a, const fp12_g<E> b) {
   const fp6_g<E> ac = fp6_mul(a.c0, b.c0);
   const fp6_g<E> bd = fp6_mul(a.c1, b.c1);
   fp12_g<E> r;
@@ -1092,13 +1092,13 @@ BLS_INLINE fp12_g<E> fp12_sqr_inl(const fp12_g<E>& f) {
 }
 
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_sqr(const fp12_g<E>& f) { return fp12_sqr_inl(f); }
+BLS_NOINLINE fp12_g<E> fp12_sqr(const fp12_g<E> f) { return fp12_sqr_inl(f); }
 
 template <class E>
 BLS_INLINE fp12_g<E> fp12_conj(const fp12_g<E>& a) { fp12_g<E> r; r.c0 = a.c0; r.c1 = fp6_neg(a.c1); return r; }
 
 template <class E>
-BLS_HD inline fp12_g<E> fp12_inv(const fp12_g<E>& f) {
+BLS_HD inline fp12_g<E> fp12_inv(const fp12_g<E> f) {
   const fp6_g<E> t = fp6_sub(fp6_mul(f.c0, f.c0), fp6_mul_by_v(fp6_mul(f.c1, f.c1)));
   const fp6_g<E> ti = fp6_inv(t);
   fp12_g<E> r;
@@ -1109,7 +1109,7 @@ BLS_HD inline fp12_g<E> fp12_inv(const fp12_g<E>& f) {
 
 // f^(q^p), p in {1,2,3}; coefficient of w^k picks up gamma[p][k] (and conj for odd p)
 template <class E>
-BLS_HD inline fp12_g<E> fp12_frob(const fp12_g<E>& f, int p) {
+BLS_HD inline fp12_g<E> fp12_frob(const fp12_g<E> f, int p) {
   const fp2_t* g = FROB_GAMMA_M[p - 1];
   const bool odd = (p & 1) != 0;
   auto fr = [&](const E& c, int k) -> E {
@@ -1163,7 +1163,7 @@ BLS_INLINE fp12_g<E> fp12_mul_by_line_inl(const fp12_g<E>& f, const E& c0, const
 }
 
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E>& f, const E& c0, const E& c1, const E& c2) {
+BLS_NOINLINE fp12_g<E> fp12_mul_by_line(const fp12_g<E> f, const E c0, const E c1, const E c2) {
   return fp12_mul_by_line_inl(f, c0, c1, c2);
 }
 
@@ -1202,6 +1202,6 @@ BLS_INLINE fp12_g<E> fp12_cyclotomic_sqr_inl(const fp12_g<E>& f) {
 }
 
 template <class E>
-BLS_NOINLINE fp12_g<E> fp12_cyclotomic_sqr(const fp12_g<E>& f) { return fp12_cyclotomic_sqr_inl(f); }
+BLS_NOINLINE fp12_g<E> fp12_cyclotomic_sqr(const fp12_g<E> f) { return fp12_cyclotomic_sqr_inl(f); }
 
 }  // namespace bls381

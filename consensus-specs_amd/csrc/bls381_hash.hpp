@@ -18,7 +18,7 @@ BLS_CONST uint32_t SHA256_K[64] = {
 BLS_INLINE uint32_t rotr32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
 // one compression of a 16-word big-endian block into state h[8]
-BLS_HD inline void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
+BLS_DEV_INLINE void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
   uint32_t w[64];
   for (int i = 0; i < 16; ++i) w[i] = blk[i];
   for (int i = 16; i < 64; ++i) {
@@ -40,7 +40,7 @@ BLS_HD inline void sha256_compress(uint32_t h[8], const uint32_t blk[16]) {
 }
 
 // SHA-256 of an arbitrary byte string (multi-block), digest as 8 big-endian words
-BLS_HD inline void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
+BLS_DEV_INLINE void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
   uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
   const uint64_t bitlen = (uint64_t)len * 8;
@@ -68,7 +68,7 @@ BLS_HD inline void sha256(uint32_t out[8], const uint8_t* msg, uint32_t len) {
 // SHA-256 of msg || dom8 || tag (mlen + 9 bytes), the input of hash_to_G2's two
 // coordinate hashes (bls_signature.md:76-77), read straight from msg: no copy,
 // no per-lane buffer, so the message may be any length.
-BLS_HD inline void sha256_msg_dom_tag(uint32_t out[8], const uint8_t* msg, uint32_t mlen, const uint8_t dom8[8],
+BLS_DEV_INLINE void sha256_msg_dom_tag(uint32_t out[8], const uint8_t* msg, uint32_t mlen, const uint8_t dom8[8],
                                       uint8_t tag) {
   uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
@@ -117,7 +117,7 @@ BLS_INLINE E g2_select_root(const E& y) {
 
 // try-and-increment part of hash_to_G2 (bls_signature.md:74-86), before the cofactor.
 // msg may be any length (py_ecc hashes any bytes); dom8 = 8 domain bytes.
-BLS_HD inline int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, uint32_t mlen,
+BLS_DEV_INLINE int hash_to_g2_candidate(aff_t<fp2_t>& out, const uint8_t* msg, uint32_t mlen,
                                        const uint8_t dom8[8]) {
   uint32_t d[8];
   sha256_msg_dom_tag(d, msg, mlen, dom8, 1);
@@ -166,7 +166,7 @@ BLS_INLINE jac_t<E> g2_psi_jac(const jac_t<E>& p) {
 // made affine first (one Fp2 inversion, a binary-xgcd Fp inverse): each of the
 // NAF's additions is then a mixed addition (7M + 4S instead of 11M + 5S).
 template <class E>
-BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E>& S) {
+BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E> S) {
   aff_t<E> a;
   if (!jac_to_aff(a, S)) return S;   // S = O: [e0] O = O
   aff_t<E> na;
@@ -189,7 +189,7 @@ BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E>& S) {
 // pairing is bilinear in its G2 argument for any G1-side point; tested against
 // every torsion fixture).  Skips the [e0]S - T step of g2_mul_cofactor.
 template <class E>
-BLS_NOINLINE jac_t<E> g2_mul_bp(const aff_t<E>& p) {
+BLS_NOINLINE jac_t<E> g2_mul_bp(const aff_t<E> p) {
   aff_t<E> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
@@ -200,7 +200,7 @@ BLS_NOINLINE jac_t<E> g2_mul_bp(const aff_t<E>& p) {
 }
 
 template <class E>
-BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
+BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E> p) {
   const jac_t<E> Q0 = g2_mul_bp(p);
   const jac_t<E> Q1 = jac_neg(g2_psi_jac(Q0));
   const jac_t<E> Q2 = jac_neg(g2_psi_jac(Q1));
@@ -210,7 +210,7 @@ BLS_NOINLINE jac_t<E> g2_mul_cofactor(const aff_t<E>& p) {
 }
 
 // full hash_to_G2 for a 32-byte message; returns false only if the result is infinity
-BLS_HD inline bool hash_to_g2_aff(aff_t<fp2_t>& out, const uint8_t msg[32], const uint8_t dom8[8]) {
+BLS_DEV_INLINE bool hash_to_g2_aff(aff_t<fp2_t>& out, const uint8_t msg[32], const uint8_t dom8[8]) {
   aff_t<fp2_t> c;
   hash_to_g2_candidate(c, msg, 32, dom8);
   return jac_to_aff(out, g2_mul_cofactor(c));

@@ -50,15 +50,23 @@ constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 #endif
 
 // ------------------------------------------------------------ SoA access --
+// Every SoA buffer is device global memory: the accesses go through global-address-space
+// pointers, so they compile to global_load / global_store even inside a non-inlined function
+// whose pointer parameter the compiler cannot trace to a kernel argument (a generic pointer
+// would make them flat accesses, which also count against lgkmcnt and wait with LDS traffic).
+typedef __attribute__((address_space(1))) const uint32_t g_cu32;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
 __device__ __forceinline__ fp_t soa_ld(const uint32_t* __restrict__ p, size_t n, size_t i, int c) {
+  g_cu32* g = (g_cu32*)p;
   fp_t r;
 #pragma unroll
-  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = p[(size_t)(c * FP_LIMBS + k) * n + i];
+  for (int k = 0; k < FP_LIMBS; ++k) r.w[k] = g[(size_t)(c * FP_LIMBS + k) * n + i];
   return r;
 }
 __device__ __forceinline__ void soa_st(uint32_t* __restrict__ p, size_t n, size_t i, int c, const fp_t& a) {
+  g_u32* g = (g_u32*)p;
 #pragma unroll
-  for (int k = 0; k < FP_LIMBS; ++k) p[(size_t)(c * FP_LIMBS + k) * n + i] = a.w[k];
+  for (int k = 0; k < FP_LIMBS; ++k) g[(size_t)(c * FP_LIMBS + k) * n + i] = a.w[k];
 }
 __device__ __forceinline__ aff_t<fp_t> soa_ld_g1(const uint32_t* p, size_t n, size_t i) {
   aff_t<fp_t> a; a.x = soa_ld(p, n, i, 0); a.y = soa_ld(p, n, i, 1); return a;
@@ -461,7 +469,7 @@ __device__ __forceinline__ void quad_line_pair(const fp2p_t& x0, const fp2p_t& x
 __device__ __forceinline__ void soa_st_L(uint32_t* __restrict__ p, size_t n, size_t i, int c, const fp_t& a) {
 #if BLS_ML_L_NT
 #pragma unroll
-  for (int k = 0; k < FP_LIMBS; ++k) __builtin_nontemporal_store(a.w[k], &p[(size_t)(c * FP_LIMBS + k) * n + i]);
+  for (int k = 0; k < FP_LIMBS; ++k) __builtin_nontemporal_store(a.w[k], &((g_u32*)p)[(size_t)(c * FP_LIMBS + k) * n + i]);
 #else
   soa_st(p, n, i, c, a);
 #endif
@@ -476,10 +484,11 @@ __device__ __forceinline__ void ml_store_L(uint32_t* __restrict__ L, size_t cnt,
 }
 
 // the 68 steps of one half's running point, with the quad's line products written to L
-__device__ __noinline__ void ml_lines_run(const aff_t<fp2p_t>& Q, const g1_line_pre& pre, bool active,
-                                         uint32_t* __restrict__ L, size_t cnt, size_t li, g2_proj<fp2p_t>& T) {
+__device__ __noinline__ g2_proj<fp2p_t> ml_lines_run(const aff_t<fp2p_t> Q, const g1_line_pre pre, bool active,
+                                                    uint32_t* __restrict__ L, size_t cnt, size_t li) {
   const bool hi = qd_hi();
   const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
+  g2_proj<fp2p_t> T;
   T.x = Q.x; T.y = Q.y; T.z = one;
   int j = 0;
   for (int b = 62; b >= 0; --b) {
@@ -493,6 +502,7 @@ __device__ __noinline__ void ml_lines_run(const aff_t<fp2p_t>& Q, const g1_line_
       ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
     }
   }
+  return T;
 }
 
 // BLS_ML_LINES_LDS=1: the doubling steps' line constants (-3 xp, 2 yp: 28 words per lane) live in
@@ -502,11 +512,6 @@ __device__ __noinline__ void ml_lines_run(const aff_t<fp2p_t>& Q, const g1_line_
 // them through flat loads at every step: most of k_ml_lines' HBM traffic beyond L itself.
 #ifndef BLS_ML_LINES_LDS
 #define BLS_ML_LINES_LDS 1
-#endif
-// BLS_ML_LINES_TLOCAL=1: the running point in the loop's own registers (written back at the
-// end) instead of the caller's frame
-#ifndef BLS_ML_LINES_TLOCAL
-#define BLS_ML_LINES_TLOCAL 1
 #endif
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 // where a half's pair lives: Q (pair SoA of nq2 lanes, lane lp), P (G1 SoA of np items, item
@@ -557,15 +562,12 @@ __device__ __forceinline__ void ml_lds_put(lds_u32* col, const g1_line_pre& pre)
 }
 // src by value: the L stores cannot alias it (a by-reference src would be re-read from the
 // caller's frame after every store)
-__device__ __noinline__ void ml_lines_run_lds(const ml_src src, const lds_u32* col, bool active,
-                                             uint32_t* __restrict__ L, size_t cnt, size_t li, g2_proj<fp2p_t>& T_out) {
+// (the final running point is returned by value: no pointer into the caller's frame)
+__device__ __noinline__ g2_proj<fp2p_t> ml_lines_run_lds(const ml_src src, const lds_u32* col, bool active,
+                                                        uint32_t* __restrict__ L, size_t cnt, size_t li) {
   const bool hi = qd_hi();
   const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
-#if BLS_ML_LINES_TLOCAL
   g2_proj<fp2p_t> T;
-#else
-  g2_proj<fp2p_t>& T = T_out;
-#endif
   {
     const aff_t<fp2p_t> Q = ml_src_q(src);
     T.x = Q.x; T.y = Q.y; T.z = one;
@@ -591,9 +593,7 @@ __device__ __noinline__ void ml_lines_run_lds(const ml_src src, const lds_u32* c
       ml_store_L(L, cnt, li, j++, hi, o0, o1, o2);
     }
   }
-#if BLS_ML_LINES_TLOCAL
-  T_out = T;
-#endif
+  return T;
 }
 
 // items i0 .. i0 + cnt - 1 of the batch (SoA inputs of n items); L and st_out are chunk-local
@@ -625,7 +625,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
   lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
   const ml_src src{qsrc, 2 * n, lp, use_pk ? pk_aff : nullptr, n, i};
   ml_lds_put(col, g1_prepare(ml_src_p(src)));   // each lane writes and reads only its own column
-  ml_lines_run_lds(src, col, active, L, cnt, li, T);
+  T = ml_lines_run_lds(src, col, active, L, cnt, li);
   const aff_t<fp2p_t> Q = ml_src_q(src);
 #else
   aff_t<fp2p_t> Q;
@@ -638,7 +638,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
     P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
   }
   const g1_line_pre pre = g1_prepare(P);
-  ml_lines_run(Q, pre, active, L, cnt, li, T);
+  T = ml_lines_run(Q, pre, active, L, cnt, li);
 #endif
   // py_ecc's zero pairing value for a degenerate loop; the strict policy's G2 test of the
   // signature on the lo half's final point (psi(sig) == -[|x|] sig)
@@ -1306,13 +1306,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(siz
   lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
   const ml_src src{h_aff, 2 * n, lp, r1_aff, n, i};
   ml_lds_put(col, g1_prepare(ml_src_p(src)));
-  ml_lines_run_lds(src, col, active, L, cnt, lq, T);
+  T = ml_lines_run_lds(src, col, active, L, cnt, lq);
 #else
   aff_t<fp2p_t> Q;
   Q.x = pr_make(soa_ld(h_aff, 2 * n, lp, 0));
   Q.y = pr_make(soa_ld(h_aff, 2 * n, lp, 1));
   const g1_line_pre pre = g1_prepare(soa_ld_g1(r1_aff, n, i));
-  ml_lines_run(Q, pre, active, L, cnt, lq, T);
+  T = ml_lines_run(Q, pre, active, L, cnt, lq);
 #endif
   bool bad = active && fp2_is_zero(T.z);
   bad = !qd_all(!bad);
@@ -1651,11 +1651,14 @@ __global__ void __launch_bounds__(KBLOCK) k_gather_field(size_t n, const uint8_t
 }
 
 // ------------------------------------------------------- sign / privtopub --
-__device__ __forceinline__ void scalar_limbs_from_be32(uint32_t k[8], const uint8_t* b) {
+__device__ __forceinline__ scalar_t scalar_from_be32(const uint8_t* b) {
+  scalar_t k;
   for (int i = 0; i < 8; ++i) {
     const uint8_t* p = b + 28 - 4 * i;
-    k[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+    k.w[i] = ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
   }
+  for (int i = 8; i < 16; ++i) k.w[i] = 0;
+  return k;
 }
 
 // sign = [sk] hash_to_G2(m, d), compressed; one lane pair per item
@@ -1672,20 +1675,16 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_sign(size_t n, con
   if (!jac_to_aff(h, g2_mul_cofactor(c))) {
     g2_compress(out + 96 * i, jac_infinity<fp2p_t>());
   } else {
-    uint32_t k[8];
-    scalar_limbs_from_be32(k, sks + 32 * i);
-    g2_compress(out + 96 * i, jac_mul_limbs(h, k, 256));
+    g2_compress(out + 96 * i, jac_mul_limbs(h, scalar_from_be32(sks + 32 * i), 256));
   }
 }
 
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_privtopub(size_t n, const uint8_t* __restrict__ sks, uint8_t* __restrict__ out) {
   const size_t i = item_index<1>();
   if (i >= n) return;
-  uint32_t k[8];
-  scalar_limbs_from_be32(k, sks + 32 * i);
   aff_t<fp_t> g; g.x = G1_GEN_X_M; g.y = G1_GEN_Y_M;
   uint8_t pk[48];
-  g1_compress(pk, jac_mul_limbs(g, k, 256));
+  g1_compress(pk, jac_mul_limbs(g, scalar_from_be32(sks + 32 * i), 256));
   for (int b = 0; b < 48; ++b) out[48 * i + b] = pk[b];
 }
 
@@ -1718,7 +1717,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_out(size_t
 template <class E> struct proj2 { E x, y, z; };
 
 template <class E>
-__device__ inline proj2<E> pyecc_double(const proj2<E>& p) {
+__device__ __forceinline__ proj2<E> pyecc_double(const proj2<E>& p) {
   const E W = fp2_mul_small(fp2_sqr(p.x), 3);
   const E S = fp2_mul(p.y, p.z);
   const E B = fp2_mul(fp2_mul(p.x, p.y), S);
@@ -1732,7 +1731,7 @@ __device__ inline proj2<E> pyecc_double(const proj2<E>& p) {
 }
 
 template <class E>
-__device__ inline proj2<E> pyecc_add(const proj2<E>& p1, const proj2<E>& p2) {
+__device__ __forceinline__ proj2<E> pyecc_add(const proj2<E>& p1, const proj2<E>& p2) {
   if (fp2_is_zero(p1.z) || fp2_is_zero(p2.z)) return fp2_is_zero(p2.z) ? p1 : p2;
   const E U1 = fp2_mul(p2.y, p1.z);
   const E U2 = fp2_mul(p1.y, p2.z);

@@ -34,6 +34,13 @@ BLS_INLINE void wz_init(wide_t& T) {
   for (int j = 0; j < 14; ++j) T.c[13 + j] = (int64_t)Q_LIMBS[j] << WIDE_OFF_SHIFT;
 }
 
+// BLS_LAZY_CSQR_V2 (default 1; 0 = the round-4 form, measurement knob): the compressed
+// squaring's column offsets ride on each column's first product (wmac_init) and u = b0 -+ b1
+// of lz_sqr_xisqr is squared unreduced (signed limbs)
+#ifndef BLS_LAZY_CSQR_V2
+#define BLS_LAZY_CSQR_V2 1
+#endif
+
 // T += x y  (signed limbs)
 BLS_INLINE void wmac(wide_t& T, const lv_t& x, const lv_t& y) {
   BLS_COUNT_MACS(196);
@@ -41,6 +48,29 @@ BLS_INLINE void wmac(wide_t& T, const lv_t& x, const lv_t& y) {
   for (int i = 0; i < 14; ++i)
 #pragma unroll
     for (int j = 0; j < 14; ++j) T.c[i + j] += (int64_t)x[i] * (int64_t)y[j];
+}
+
+// T = x y + the offset of wz_init: each column's first product takes the column's initial
+// value as its addend (one v_mad with a scalar operand) instead of a separate move
+BLS_INLINE void wmac_init(wide_t& T, const lv_t& x, const lv_t& y) {
+#if !BLS_LAZY_CSQR_V2
+  wz_init(T);
+  wmac(T, x, y);
+  return;
+#endif
+  BLS_COUNT_MACS(196);
+#pragma unroll
+  for (int i = 0; i < 14; ++i)
+#pragma unroll
+    for (int j = 0; j < 14; ++j) {
+      const int k = i + j;
+      const int64_t p = (int64_t)x[i] * (int64_t)y[j];
+      if (i == 0 || j == 13)   // column k's first product in this order
+        T.c[k] = p + ((k >= 13) ? ((int64_t)Q_LIMBS[k - 13] << WIDE_OFF_SHIFT) : 0);
+      else
+        T.c[k] += p;
+    }
+  T.c[27] = 0;
 }
 
 // T += k x^2 for a small signed k (105 products: cross terms doubled in the multiplier)
@@ -124,8 +154,7 @@ BLS_INLINE fp_t lz_xi_mul(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0
     y2[k] = p ? d : -s;
   }
   wide_t T;
-  wz_init(T);
-  wmac(T, x1, y1);
+  wmac_init(T, x1, y1);
   wmac(T, x2, y2);
   return wredc(T);
 }
@@ -141,32 +170,40 @@ BLS_INLINE fp_t lz_mul(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0, c
     y2[k] = p ? (int32_t)b0.w[k] : -(int32_t)b1.w[k];
   }
   wide_t T;
-  wz_init(T);
-  wmac(T, x1, y1);
+  wmac_init(T, x1, y1);
   wmac(T, x2, y2);
   return wredc(T);
 }
 
 // Re/Im of a^2 + xi b^2, with the xi b^2 part as squares:
 //   Re(xi b^2) = (b0 - b1)^2 - 2 b1^2,  Im(xi b^2) = (b0 + b1)^2 - 2 b1^2
-// (u = b0 -+ b1 reduced first, so its square's columns stay small): 196 + 105 + 105
-// products per lane instead of 3 x 196.  Columns: a-term 14 x 2^57, u^2 7.5 x 2^57,
-// 2 b1^2 7.5 x 2^58, reduction 14 x 2^56: < 2^62.5.  Values in (-16 q^2, 12 q^2).
+// 196 + 105 + 105 products per lane instead of 3 x 196.  u = b0 -+ b1 is squared as signed
+// limbs, unreduced (round 5; it was reduced mod 2q first): |u_k| < 2^28 (lane 0) or
+// u_k < 2^29 (lane 1).  Columns, lane 1 (all terms but 2 b1^2 non-negative): a-term
+// 14 x 2^57 + u^2 15 x 2^58 + reduction 14 x 2^56 < 2^62.7, and -2 b1^2 > -2^60.9; lane 0 is
+// smaller.  Values: lane 0 in (-16 q^2, 12 q^2), lane 1 in (-8 q^2, 24 q^2) (u < 4q), inside
+// wredc's (-q 2^386, 2^390 q) ~ (-42 q^2, 675 q^2).
 BLS_INLINE fp_t lz_sqr_xisqr(bool p, const fp_t& a0, const fp_t& a1, const fp_t& b0, const fp_t& b1) {
   lv_t x1, y1, u, v;
-  uint32_t s[14];
 #pragma unroll
   for (int k = 0; k < 14; ++k) {
     const int32_t e = (int32_t)a0.w[k], o = (int32_t)a1.w[k];
     x1[k] = e + (p ? e : o);
     y1[k] = p ? o : e - o;
-    s[k] = b0.w[k] + (p ? b1.w[k] : Q2B_LIMBS[k] - b1.w[k]);
-    v[k] = (int32_t)b1.w[k];
+    const int32_t c = (int32_t)b0.w[k], d = (int32_t)b1.w[k];
+    u[k] = p ? c + d : c - d;
+    v[k] = d;
   }
-  lv_from(u, fp_reduce_lc<2>(s));
+#if !BLS_LAZY_CSQR_V2
+  {
+    uint32_t s[14];
+#pragma unroll
+    for (int k = 0; k < 14; ++k) s[k] = b0.w[k] + (p ? b1.w[k] : Q2B_LIMBS[k] - b1.w[k]);
+    lv_from(u, fp_reduce_lc<2>(s));
+  }
+#endif
   wide_t T;
-  wz_init(T);
-  wmac(T, x1, y1);
+  wmac_init(T, x1, y1);
   wsqr_k(T, u, 1);
   wsqr_k(T, v, -2);
   return wredc(T);

@@ -232,7 +232,7 @@ __device__ __forceinline__ cyc_bc<fp2p_t> cyc_csqr_lazy(const cyc_bc<fp2p_t>& g)
 }
 
 // 1/a = conj(a) / (a0^2 + a1^2); the norm and its inverse are computed on both lanes
-__device__ inline fp2p_t fp2_inv(const fp2p_t& a) {
+__device__ inline fp2p_t fp2_inv(const fp2p_t a) {
   const fp_t t = fp_sqr(a.v);
   const fp_t ni = fp_inv(fp_add(t, pr_dpp<DPP_SWAP>(t)));
   const fp_t r = fp_mul(a.v, ni);
@@ -244,7 +244,7 @@ __device__ inline fp2p_t fp2_inv(const fp2p_t& a) {
 // and delta = (a0 + gamma)/2 (both lanes), t = delta^((q+1)/4) and 1/t come
 // from one power of delta; the root is (t, a1/(2t)) when t^2 = delta and
 // (a1/(2t), t) otherwise.
-__device__ inline bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
+__device__ __forceinline__ bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
   const bool odd = pr_odd();
   const fp_t a0 = pr_dpp<DPP_EVEN>(a.v);
   const fp_t a1 = pr_dpp<DPP_ODD>(a.v);
@@ -298,7 +298,7 @@ __device__ __forceinline__ int g2_y_flag(const fp2p_t& y_mont) {
 
 // G2 decompress (bls_signature.md:54-64 / py_ecc decompress_G2, bls381_curve.hpp):
 // z1 = flags | x_im (odd lane), z2 = x_re (even lane; lax: all 384 bits, reduced mod q)
-__device__ inline int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96, bool lax) {
+__device__ __forceinline__ int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96, bool lax) {
   const bool odd = pr_odd();
   const uint8_t top = b96[0];
   const int b1 = (top >> 6) & 1, a1 = (top >> 5) & 1;
@@ -321,7 +321,7 @@ __device__ inline int g2_decompress(aff_t<fp2p_t>& out, const uint8_t* b96, bool
 }
 
 // each lane writes its 48-byte half of the 96-byte encoding at out96
-__device__ inline void g2_compress_aff(uint8_t* out96, const aff_t<fp2p_t>& a) {
+__device__ __forceinline__ void g2_compress_aff(uint8_t* out96, const aff_t<fp2p_t>& a) {
   const bool odd = pr_odd();
   const int flag = g2_y_flag(a.y);
   uint8_t b[48];
@@ -331,7 +331,7 @@ __device__ inline void g2_compress_aff(uint8_t* out96, const aff_t<fp2p_t>& a) {
   for (int i = 0; i < 48; ++i) dst[i] = b[i];
 }
 
-__device__ inline void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
+__device__ __forceinline__ void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
   aff_t<fp2p_t> a;
   if (!jac_to_aff(a, p)) {
     const bool odd = pr_odd();
@@ -348,7 +348,7 @@ __device__ inline void g2_compress(uint8_t* out96, const jac_t<fp2p_t>& p) {
 // hashes m || dom8 || 0x01 (x_re), the odd lane m || dom8 || 0x02 (x_im).
 // known_k >= 0: the candidate offset is already known (k_hash_search found the first
 // square, x + known_k), so the Legendre search is skipped.
-__device__ inline int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* msg, uint32_t mlen,
+__device__ __forceinline__ int hash_to_g2_candidate(aff_t<fp2p_t>& out, const uint8_t* msg, uint32_t mlen,
                                            const uint8_t dom8[8], int known_k = -1) {
   const bool odd = pr_odd();
   uint32_t d[8];

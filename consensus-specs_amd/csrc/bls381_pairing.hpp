@@ -36,12 +36,12 @@ template <class E> struct g2_proj { E x, y, z; };
 
 // the doubling step reads only -3 xp and 2 yp, through these accessors: a kernel may keep
 // them elsewhere than in a g1_line_pre (k_ml_lines: in LDS)
-BLS_HD inline const fp_t& pre_n3x(const g1_line_pre& p) { return p.n3x; }
-BLS_HD inline const fp_t& pre_y2(const g1_line_pre& p) { return p.y2; }
+BLS_DEV_INLINE const fp_t& pre_n3x(const g1_line_pre& p) { return p.n3x; }
+BLS_DEV_INLINE const fp_t& pre_y2(const g1_line_pre& p) { return p.y2; }
 
 // doubling step: T <- 2T, returns the tangent line at the old T evaluated at P
 template <class E, class PRE>
-BLS_HD inline void line_dbl(g2_proj<E>& T, const PRE& P, E& c0, E& c1, E& c2) {
+BLS_DEV_INLINE void line_dbl(g2_proj<E>& T, const PRE& P, E& c0, E& c1, E& c2) {
   const E XX = fp2_sqr(T.x);
   const E YY = fp2_sqr(T.y);
   const E ZZ = fp2_sqr(T.z);
@@ -63,7 +63,7 @@ BLS_HD inline void line_dbl(g2_proj<E>& T, const PRE& P, E& c0, E& c1, E& c2) {
 
 // addition step: T <- T + Q, returns the chord through T and Q evaluated at P
 template <class E>
-BLS_HD inline void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre& P, E& c0, E& c1, E& c2) {
+BLS_DEV_INLINE void line_add(g2_proj<E>& T, const aff_t<E>& Q, const g1_line_pre& P, E& c0, E& c1, E& c2) {
   const E u = fp2_sub(fp2_mul(Q.y, T.z), T.y);
   const E v = fp2_sub(fp2_mul(Q.x, T.z), T.x);
   c0 = fp2_sub(fp2_mul(u, Q.x), fp2_mul(v, Q.y));
@@ -152,9 +152,16 @@ BLS_INLINE fp12_g<E> fp12_mul_by_line_pair_inl(const fp12_g<E>& f, const fp12_g<
 // T0_out != nullptr: receives the first pair's final running point, [|x|] Q[0] in
 // homogeneous projective coordinates (the signature's G2 membership test rides on it,
 // g2_psi_matches_neg).
+// The loop itself takes its pairs and returns its results by value (miller_loop_run): no
+// pointer into the caller's private memory crosses the call; the pointer
+// form below is a force-inlined wrapper over the caller's own arrays.
+template <int N, class E> struct ml_pairs { aff_t<E> Q[N]; g1_line_pre P[N]; };
+template <class E> struct ml_result { fp12_g<E> f; g2_proj<E> T0; bool degenerate; };
+
 template <int N, class E>
-BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bool& degenerate,
-                                     g2_proj<E>* T0_out = nullptr) {
+BLS_NOINLINE ml_result<E> miller_loop_run(const ml_pairs<N, E> in) {
+  const aff_t<E>* Q = in.Q;
+  const g1_line_pre* P = in.P;
   g2_proj<E> T[N];
   for (int k = 0; k < N; ++k) { T[k].x = Q[k].x; T[k].y = Q[k].y; T[k].z = e2_one<E>(); }
   fp12_g<E> f = fp12_one<E>();
@@ -195,15 +202,28 @@ BLS_NOINLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bo
   }
   bool deg = false;
   for (int k = 0; k < N; ++k) deg = deg | fp2_is_zero(T[k].z);   // no short circuit: pair-uniform DPP
-  degenerate = deg;
-  if (T0_out) *T0_out = T[0];
-  return fp12_conj(f);
+  ml_result<E> r;
+  r.f = fp12_conj(f);
+  r.T0 = T[0];
+  r.degenerate = deg;
+  return r;
+}
+
+template <int N, class E>
+BLS_DEV_INLINE fp12_g<E> miller_loop_n(const aff_t<E>* Q, const g1_line_pre* P, bool& degenerate,
+                                   g2_proj<E>* T0_out = nullptr) {
+  ml_pairs<N, E> in;
+  for (int k = 0; k < N; ++k) { in.Q[k] = Q[k]; in.P[k] = P[k]; }
+  const ml_result<E> r = miller_loop_run<N, E>(in);
+  degenerate = r.degenerate;
+  if (T0_out) *T0_out = r.T0;
+  return r.f;
 }
 
 // G2 membership from a Miller loop's by-product: Q in G2 iff psi(Q) == [x] Q = -[|x|] Q, and
 // the loop's final running point T (homogeneous projective, Z != 0) is [|x|] Q.
 template <class E>
-BLS_HD inline bool g2_psi_matches_neg(const aff_t<E>& q, const g2_proj<E>& T) {
+BLS_DEV_INLINE bool g2_psi_matches_neg(const aff_t<E>& q, const g2_proj<E>& T) {
   const aff_t<E> s = g2_psi(q);
   const bool a = fp2_eq(fp2_mul(s.x, T.z), T.x);
   const bool b = fp2_eq(fp2_mul(s.y, T.z), fp2_neg(T.y));
@@ -212,7 +232,7 @@ BLS_HD inline bool g2_psi_matches_neg(const aff_t<E>& q, const g2_proj<E>& T) {
 
 // runtime pair count (for verify_multiple chunks); pairs processed one at a time
 template <class E>
-BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P, bool& degenerate) {
+BLS_DEV_INLINE fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P, bool& degenerate) {
   return miller_loop_n<1>(&Q, &P, degenerate);
 }
 
@@ -224,7 +244,7 @@ BLS_HD inline fp12_g<E> miller_loop_1(const aff_t<E>& Q, const g1_line_pre& P, b
 BLS_CONST int CYC_X_RUNS[6] = {1, 2, 3, 9, 32, 16};
 
 template <class E>
-BLS_NOINLINE fp12_g<E> cyc_exp_x_gs(const fp12_g<E>& f) {
+BLS_NOINLINE fp12_g<E> cyc_exp_x_gs(const fp12_g<E> f) {
   fp12_g<E> r = f;
   for (int s = 0; s < 6; ++s) {
     for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fp12_cyclotomic_sqr_inl(r);
@@ -338,7 +358,7 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 
 #if BLS_CYC_TAIL_GS
 template <class E>
-BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
   BLS_FE_MARK(7);
   cyc_bc<E> snap[3];
   cyc_bc<E> g = cyc_compress(f);
@@ -373,7 +393,7 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
 }
 #else
 template <class E>
-BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
+BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
   cyc_bc<E> snap[6];
   cyc_bc<E> g = cyc_compress(f);
   bool zero = false;
@@ -404,7 +424,7 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E>& f) {
 // reduced pairing value is 1 (DESIGN.md "Final exponentiation").
 // Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3.
 template <class E>
-BLS_HD inline fp12_g<E> final_exp(const fp12_g<E>& f) {
+BLS_HD inline fp12_g<E> final_exp(const fp12_g<E> f) {
   fp12_g<E> t = FE_MUL12(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
   t = FE_MUL12(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
   BLS_FE_MARK(5);

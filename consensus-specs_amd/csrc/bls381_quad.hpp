@@ -132,13 +132,15 @@ __device__ __forceinline__ fq12_t fq12_two_lines(const fp2p_t& x0, const fp2p_t&
 #ifndef BLS_ML_QUAD_INLINE
 #define BLS_ML_QUAD_INLINE 0
 #endif
+// (operands and results by value: no pointer into the caller's private memory crosses the
+// call; the reference form below is a force-inlined wrapper)
+struct fq12_ml { fq12_t f; bool degenerate; };
 #if BLS_ML_QUAD_INLINE
 __device__ __forceinline__
 #else
 __device__ __noinline__
 #endif
-fq12_t miller_loop_quad(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool active,
-                                                bool& degenerate) {
+fq12_ml miller_loop_quad_run(const aff_t<fp2p_t> Q, const g1_line_pre P, bool active) {
   g2_proj<fp2p_t> T;
   T.x = Q.x; T.y = Q.y; T.z = e2_one<fp2p_t>();
   const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
@@ -156,8 +158,17 @@ fq12_t miller_loop_quad(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool activ
     }
   }
   const bool deg = active && fp2_is_zero(T.z);
-  degenerate = !qd_all(!deg);
-  return fq12_conj(f);
+  fq12_ml r;
+  r.degenerate = !qd_all(!deg);
+  r.f = fq12_conj(f);
+  return r;
+}
+
+__device__ __forceinline__ fq12_t miller_loop_quad(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool active,
+                                                   bool& degenerate) {
+  const fq12_ml r = miller_loop_quad_run(Q, P, active);
+  degenerate = r.degenerate;
+  return r.f;
 }
 
 // ------------------------------------------------ one Miller pair per quad --
@@ -263,7 +274,7 @@ __device__ __forceinline__ fq12_t fq12_mul_by_line_q1(const fq12_t& f, const fp2
 }
 
 // Miller loop of one pair on a quad; returns conj(f) (x < 0).  degenerate as in miller_loop_n.
-__device__ __noinline__ fq12_t miller_loop_q1(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool& degenerate) {
+__device__ __noinline__ fq12_ml miller_loop_q1_run(const aff_t<fp2p_t> Q, const g1_line_pre P) {
   g2_proj<fp2p_t> T;
   T.x = Q.x; T.y = Q.y; T.z = e2_one<fp2p_t>();
   fq12_t f = fq12_one();
@@ -279,8 +290,16 @@ __device__ __noinline__ fq12_t miller_loop_q1(const aff_t<fp2p_t>& Q, const g1_l
       f = fq12_mul_by_line_q1(f, c0, c1, c2);
     }
   }
-  degenerate = fp2_is_zero(T.z);   // T is the same on all four lanes
-  return fq12_conj(f);
+  fq12_ml r;
+  r.degenerate = fp2_is_zero(T.z);   // T is the same on all four lanes
+  r.f = fq12_conj(f);
+  return r;
+}
+
+__device__ __forceinline__ fq12_t miller_loop_q1(const aff_t<fp2p_t>& Q, const g1_line_pre& P, bool& degenerate) {
+  const fq12_ml r = miller_loop_q1_run(Q, P);
+  degenerate = r.degenerate;
+  return r.f;
 }
 
 // ------------------------------------------- final exponentiation on quads --
@@ -410,7 +429,7 @@ __device__ __forceinline__ fq12_t cq_decompress(const cq_t& g, const fp2p_t& inv
 }
 
 // exact fallback (cyc_exp_x_gs): generic squarings, valid for every element
-__device__ __noinline__ fq12_t cyc_exp_x_gs_q(const fq12_t& f) {
+__device__ __noinline__ fq12_t cyc_exp_x_gs_q(const fq12_t f) {
   fq12_t r = f;
   for (int s = 0; s < 6; ++s) {
     for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fq12_sqr(r);
@@ -420,7 +439,7 @@ __device__ __noinline__ fq12_t cyc_exp_x_gs_q(const fq12_t& f) {
 }
 
 // f^x (cyc_exp_x): compressed squarings, six snapshots, one shared inversion
-__device__ __noinline__ fq12_t cyc_exp_x_q(const fq12_t& f) {
+__device__ __noinline__ fq12_t cyc_exp_x_q(const fq12_t f) {
   const bool hi = qd_hi();
   cq_t snap[6];
   cq_t g = cq_compress(f);
@@ -452,7 +471,7 @@ __device__ __noinline__ fq12_t cyc_exp_x_q(const fq12_t& f) {
 }
 
 // f^(3 (q^12 - 1)/r), the chain of final_exp
-__device__ inline fq12_t final_exp_q(const fq12_t& f) {
+__device__ inline fq12_t final_exp_q(const fq12_t f) {
   fq12_t t = fq12_mul(fq12_conj(f), fq12_inv(f));          // f^(q^6 - 1)
   t = fq12_mul(fq12_frob(t, 2), t);                        // ^(q^2 + 1)
   fq12_t a = fq12_mul(cyc_exp_x_q(t), fq12_conj(t));       // t^(x-1)
@@ -535,7 +554,7 @@ __device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
 }
 
 // cyc_exp_x_q with the squarings on the octet
-__device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t& f) {
+__device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t f) {
   const bool hi = qd_hi();
   cq_t snap[6];
   fp2p_t g = co_enter(cq_compress(f));
@@ -566,7 +585,7 @@ __device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t& f) {
 }
 
 // final_exp_q with cyc_exp_x_o: both quads of the octet hold f
-__device__ inline fq12_t final_exp_o(const fq12_t& f) {
+__device__ inline fq12_t final_exp_o(const fq12_t f) {
   fq12_t t = fq12_mul(fq12_conj(f), fq12_inv(f));
   t = fq12_mul(fq12_frob(t, 2), t);
   fq12_t a = fq12_mul(cyc_exp_x_o(t), fq12_conj(t));

@@ -21,7 +21,7 @@ constexpr int SSZ_STACK = 64;    // chunks
 constexpr int SSZ_PROG_MAX = 512;  // u32 words
 
 // SHA-256 of two 32-byte chunks (one data block + the constant padding block)
-BLS_HD inline void sha256_pair(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
+BLS_DEV_INLINE void sha256_pair(uint32_t out[8], const uint32_t l[8], const uint32_t r[8]) {
   uint32_t h[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
                    0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
   uint32_t blk[16];
@@ -36,7 +36,7 @@ BLS_HD inline void sha256_pair(uint32_t out[8], const uint32_t l[8], const uint3
 
 // Runs `prog` over one serialized item; the root (8 big-endian words) is left in
 // root.  Returns false on a malformed program (stack over/underflow).
-BLS_HD inline bool ssz_run(uint32_t root[8], const uint8_t* item, const uint32_t* prog, uint32_t plen,
+BLS_DEV_INLINE bool ssz_run(uint32_t root[8], const uint8_t* item, const uint32_t* prog, uint32_t plen,
                            uint32_t (*stk)[8]) {
   int sp = 0;
   for (uint32_t pc = 0; pc < plen;) {

@@ -272,11 +272,16 @@ int hc_verify_batch_mt(size_t n, const uint8_t* pks, const uint8_t* msgs32, cons
 }
 
 // G1 / G2 scalar multiplication with the same curve code (fixture helpers)
+static scalar_t hc_scalar(const uint32_t* k_limbs, int nbits) {
+  scalar_t k{};
+  for (int i = 0; i < (nbits + 31) / 32 && i < 16; ++i) k.w[i] = k_limbs[i];
+  return k;
+}
 void hc_g1_mul(const uint8_t* aff96, const uint32_t* k_limbs, int nbits, uint8_t* b48) {
-  g1_compress(b48, jac_mul_limbs(ldg1(aff96), k_limbs, nbits));
+  g1_compress(b48, jac_mul_limbs(ldg1(aff96), hc_scalar(k_limbs, nbits), nbits));
 }
 void hc_g2_mul(const uint8_t* aff192, const uint32_t* k_limbs, int nbits, uint8_t* b96) {
-  g2_compress(b96, jac_mul_limbs(ldg2(aff192), k_limbs, nbits));
+  g2_compress(b96, jac_mul_limbs(ldg2(aff192), hc_scalar(k_limbs, nbits), nbits));
 }
 
 // SSZ root program (bls381_ssz.hpp) over one serialized item: 1 ok, 0 malformed program
