@@ -220,7 +220,8 @@ PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2", "decod
                   "hash_to_g2": "k_hash_g2",
                   "miller_loop_2": "k_miller_verify", "final_exp": "k_final_exp_verdict",
                   "miller_lines": "k_ml_lines", "miller_accum": "k_ml_accum",
-                  "hash_cand": "k_hash_cand_1", "hash_bp": "k_hash_bp"}
+                  "hash_cand": "k_hash_cand_1", "hash_bp": "k_hash_bp",
+                  "final_exp_q": "k_final_exp_verdict_q<1>", "miller_loop_2q": "k_miller_verify_q"}
 # the C2 batch (2^16 items) runs the split Miller loop: the monolithic count is not part of its pipeline
 PIPELINE_STAGES = ["decode_g1", "decode_g2", "hash_to_g2", "miller_lines", "miller_accum", "final_exp"]
 # the final exponentiation of the throughput path runs as six launches (BLS_FE_SPLIT): its stage is
@@ -247,7 +248,7 @@ def stage_kernels(prof_key, prof):
         return FE_SPLIT_KERNELS
     if prof_key == "decode_g2" and "decode_g2_1" in prof:
         return [(PROFILE_KERNEL["decode_g2_1"], 1)]
-    return [(PROFILE_KERNEL[prof_key], 1)]
+    return [(PROFILE_KERNEL.get(prof_key, "k_" + prof_key), 1)]
 
 
 def load_pmc_traffic(kernels, n):

@@ -213,6 +213,11 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
 // final exponentiation + verdict of n Fp12 values (lane-pair SoA): on lane quads while
 // the batch leaves SIMDs idle (k_final_exp_verdict_q: half the per-item latency, more
 // lane work), on lane pairs above that
+// BLS_ML_ACCUM_QUAD=1 (measurement knob): the throughput path's f accumulation on lane quads
+// (k_ml_accum_q: each lane holds half of f, 42 words instead of 84) instead of lane pairs
+#ifndef BLS_ML_ACCUM_QUAD
+#define BLS_ML_ACCUM_QUAD 0
+#endif
 #ifndef BLS_FE_QUAD_MAX_N
 #define BLS_FE_QUAD_MAX_N 49152
 #endif
@@ -487,8 +492,13 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
       LAUNCH("miller_lines", s, dim3(grid_for(4 * cnt)), b, k_ml_lines, n, i0, cnt, (const uint32_t*)w.sig_aff,
              (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
              w.ml_L, w.ml_st, sig_in_loop ? 1 : 0);
+#if BLS_ML_ACCUM_QUAD
+      LAUNCH("miller_accum", s, dim3(grid_for(4 * cnt)), b, k_ml_accum_q, n, i0, cnt, (const uint32_t*)w.ml_L,
+             (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);
+#else
       LAUNCH("miller_accum", s, dim3(grid_for(2 * cnt)), b, k_ml_accum, n, i0, cnt, (const uint32_t*)w.ml_L,
              (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);
+#endif
     }
   } else {
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
