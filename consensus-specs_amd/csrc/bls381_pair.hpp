@@ -231,10 +231,118 @@ __device__ __forceinline__ cyc_bc<fp2p_t> cyc_csqr_lazy(const cyc_bc<fp2p_t>& g)
   return r;
 }
 
-// 1/a = conj(a) / (a0^2 + a1^2); the norm and its inverse are computed on both lanes
+// 1/x for an x both lanes of the pair hold (the norm of an Fp2 inverse): fp_inv's optimized
+// binary GCD (bls381_field.hpp) with each round's two row updates split over the pair.  Both
+// lanes run the same 30-step inner loop on the same approximations; lane 0 then applies the row
+// (f0, g0) -- the new a and u -- and lane 1 the row (f1, g1) -- the new b and v -- and each reads
+// the other's row by DPP.  Lane-relative: X = this lane's row, Y = the partner's, so lane 0 has
+// (X, Y, U, V) = (a, b, u, v) and lane 1 (b, a, v, u), and both apply the same code with
+// (cX, cY) = (f0, g0) on lane 0 and (g1, f1) on lane 1.  Half of fp_inv's full-width work per lane.
+#ifndef BLS_INV_PAIR
+#define BLS_INV_PAIR 1
+#endif
+__device__ inline fp_t fp_inv_pair(const fp_t am) {
+  const bool odd = pr_odd();
+  uint32_t w[12];
+  fp_plain_to_words(w, fp_reduce_once(am));
+  uint32_t z = 0;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) z |= w[i];
+  if (z == 0) return fp_zero();   // both lanes of the pair hold the same x
+  int32_t A[INV_L], X[INV_L], Y[INV_L], U[INV_L], V[INV_L];
+  inv_to_l30(A, w);
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) {
+    X[i] = odd ? Q_L30[i] : A[i];
+    Y[i] = odd ? A[i] : Q_L30[i];
+    U[i] = 0;
+    V[i] = 0;
+  }
+  if (odd) V[0] = 1; else U[0] = 1;   // u = 1, v = 0
+  for (int round = 0; round < 26; ++round) {
+    int t = 2;
+    uint32_t top = 0;
+#pragma unroll
+    for (int i = 2; i < INV_L; ++i) {
+      const uint32_t c = (uint32_t)(X[i] | Y[i]);
+      if (c) { t = i; top = c; }
+    }
+    const int bl = top ? 32 - __builtin_clz(top) : 2;
+    uint32_t x2 = 0, x1 = 0, x0 = 0, y2 = 0, y1 = 0, y0 = 0;
+#pragma unroll
+    for (int i = 2; i < INV_L; ++i) {
+      const bool s = i == t;
+      x2 = s ? (uint32_t)X[i] : x2; x1 = s ? (uint32_t)X[i - 1] : x1; x0 = s ? (uint32_t)X[i - 2] : x0;
+      y2 = s ? (uint32_t)Y[i] : y2; y1 = s ? (uint32_t)Y[i - 1] : y1; y0 = s ? (uint32_t)Y[i - 2] : y0;
+    }
+    // a = lane 0's X / lane 1's Y, b the other
+    const uint32_t a2 = odd ? y2 : x2, a1 = odd ? y1 : x1, a0 = odd ? y0 : x0;
+    const uint32_t b2 = odd ? x2 : y2, b1 = odd ? x1 : y1, b0 = odd ? x0 : y0;
+    const uint32_t al0 = (uint32_t)(odd ? Y[0] : X[0]), bl0 = (uint32_t)(odd ? X[0] : Y[0]);
+    const uint32_t al1 = (uint32_t)(odd ? Y[1] : X[1]), bl1 = (uint32_t)(odd ? X[1] : Y[1]);
+    const uint32_t al2 = (uint32_t)(odd ? Y[2] : X[2]), bl2 = (uint32_t)(odd ? X[2] : Y[2]);
+    const uint64_t wa = ((uint64_t)a2 << 31) | ((uint64_t)a1 << 1) | (a0 >> 29);
+    const uint64_t wb = ((uint64_t)b2 << 31) | ((uint64_t)b1 << 1) | (b0 >> 29);
+    uint64_t xa = ((wa >> (bl - 1)) << 30) | al0;
+    uint64_t xb = ((wb >> (bl - 1)) << 30) | bl0;
+    if (t == 2 && bl <= 2) {
+      xa = al0 | ((uint64_t)al1 << 30) | ((uint64_t)al2 << 60);
+      xb = bl0 | ((uint64_t)bl1 << 30) | ((uint64_t)bl2 << 60);
+    }
+    int32_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 10
+    for (int j = 0; j < 30; ++j) {
+      const bool od = (xa & 1) != 0;
+      const bool sw = od && xa < xb;
+      const uint64_t ta = sw ? xb : xa, tb = sw ? xa : xb;
+      const int32_t tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+      xa = (od ? ta - tb : ta) >> 1;
+      xb = tb;
+      f0 = od ? tf0 - tf1 : tf0;
+      g0 = od ? tg0 - tg1 : tg0;
+      f1 = tf1 + tf1;
+      g1 = tg1 + tg1;
+    }
+    int32_t cX = odd ? g1 : f0, cY = odd ? f1 : g0;
+    int32_t nX[INV_L], nU[INV_L];
+    inv_lin_shift(nX, X, Y, cX, cY);
+    if (nX[INV_L - 1] < 0) { inv_neg(nX); cX = -cX; cY = -cY; }
+    inv_lin_modq(nU, U, V, cX, cY);
+#pragma unroll
+    for (int i = 0; i < INV_L; ++i) {
+      X[i] = nX[i];
+      Y[i] = (int32_t)pr_dpp<DPP_SWAP>((uint32_t)nX[i]);
+      U[i] = nU[i];
+      V[i] = (int32_t)pr_dpp<DPP_SWAP>((uint32_t)nU[i]);
+    }
+  }
+  // done when a == 0 and b == 1; the inverse is v (lane 0's V, lane 1's U)
+  uint32_t bad = 0;
+#pragma unroll
+  for (int i = 0; i < INV_L; ++i) {
+    const uint32_t a = (uint32_t)(odd ? Y[i] : X[i]), b = (uint32_t)(odd ? X[i] : Y[i]);
+    bad |= a | (i ? b : b ^ 1u);
+  }
+  if (BLS_ANY(bad != 0)) return fp_inv_xgcd(am);
+  fp_t r;
+#pragma unroll
+  for (int k = 0; k < 14; ++k) {
+    const int bit = 28 * k, i = bit / 30, sh = bit % 30;
+    uint64_t x = (uint64_t)(uint32_t)(odd ? U[i] : V[i]) >> sh;
+    if (i + 1 < INV_L) x |= (uint64_t)(uint32_t)(odd ? U[i + 1] : V[i + 1]) << (30 - sh);
+    r.w[k] = (uint32_t)x & FP_MASK;
+  }
+  return fp_mul(r, FP_R3);
+}
+
+// 1/a = conj(a) / (a0^2 + a1^2); the norm (the same on both lanes) is inverted by the pair
 __device__ inline fp2p_t fp2_inv(const fp2p_t a) {
   const fp_t t = fp_sqr(a.v);
+#if BLS_INV_PAIR
+  const fp_t ni = fp_inv_pair(fp_add(t, pr_dpp<DPP_SWAP>(t)));
+#else
   const fp_t ni = fp_inv(fp_add(t, pr_dpp<DPP_SWAP>(t)));
+#endif
   const fp_t r = fp_mul(a.v, ni);
   return pr_make(fp_sel(pr_odd(), fp_neg(r), r));
 }
