@@ -8,6 +8,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <vector>
+#include <unistd.h>
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
@@ -40,28 +41,38 @@ __global__ __launch_bounds__(256) void k_mad_clock(uint64_t* out, unsigned long 
 }
 
 int main(int argc, char** argv) {
+  // clock_probe [blocks] [threads per block] [idle ms before each timed launch] [launches]
   const int blocks = argc > 1 ? atoi(argv[1]) : 16384;
+  const int threads = argc > 2 ? atoi(argv[2]) : 256;
+  const int idle_ms = argc > 3 ? atoi(argv[3]) : 0;
+  const int reps = argc > 4 ? atoi(argv[4]) : 1;
+  const int wpb = (threads + 63) / 64;
   uint64_t* out;
   unsigned long long* st;
   CHECK(hipMalloc(&out, (size_t)blocks * 256 * 8));
   CHECK(hipMalloc(&st, (size_t)blocks * 4 * 2 * 8));
-  hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(256), 0, 0, out, st, 7u);
+  hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 7u);
   CHECK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  CHECK(hipEventRecord(e0, 0));
-  hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(256), 0, 0, out, st, 9u);
-  CHECK(hipEventRecord(e1, 0));
-  CHECK(hipEventSynchronize(e1));
-  float ms = 0;
-  CHECK(hipEventElapsedTime(&ms, e0, e1));
-  std::vector<unsigned long long> h((size_t)blocks * 8);
-  CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
-  double cyc = 0, rt = 0;
-  for (size_t i = 0; i < h.size(); i += 2) { cyc += (double)h[i]; rt += (double)h[i + 1]; }
-  const double macs = (double)blocks * 256 * ITERS * 8;
-  printf("{\"blocks\": %d, \"ms\": %.4f, \"mad_Tops\": %.2f, \"s_memtime_ghz\": %.3f, \"cycles_per_mad_per_wave\": %.3f}\n",
-         blocks, ms, macs / (ms * 1e-3) / 1e12, cyc / (rt * 10.0), (cyc / (blocks * 4.0)) / (ITERS * 8.0));
+  for (int r = 0; r < reps; ++r) {
+    if (idle_ms) usleep(1000 * idle_ms);
+    CHECK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 9u);
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> h((size_t)blocks * 8);
+    CHECK(hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+    double cyc = 0, rt = 0;
+    for (int b = 0; b < blocks; ++b)
+      for (int w = 0; w < wpb; ++w) { cyc += (double)h[((size_t)b * 4 + w) * 2]; rt += (double)h[((size_t)b * 4 + w) * 2 + 1]; }
+    const double macs = (double)blocks * threads * ITERS * 8;
+    printf("{\"blocks\": %d, \"threads\": %d, \"idle_ms\": %d, \"ms\": %.4f, \"mad_Tops\": %.3f, \"s_memtime_ghz\": %.3f, "
+           "\"cycles_per_mad_per_wave\": %.3f}\n", blocks, threads, idle_ms, ms, macs / (ms * 1e-3) / 1e12, cyc / (rt * 10.0),
+           (cyc / ((double)blocks * wpb)) / (ITERS * 8.0));
+  }
   return 0;
 }
