@@ -61,32 +61,36 @@ __global__ __launch_bounds__(256) void k_mac(uint64_t* out, uint32_t seed) {
 }
 
 template <int V>
-static void run(const char* name, uint64_t* out, int blocks, int macs_per_iter) {
-  hipLaunchKernelGGL((k_mac<V>), dim3(blocks), dim3(256), 0, 0, out, 7u);
+static void run(const char* name, uint64_t* out, int blocks, int threads, int macs_per_iter) {
+  hipLaunchKernelGGL((k_mac<V>), dim3(blocks), dim3(threads), 0, 0, out, 7u);
   CHECK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   CHECK(hipEventRecord(e0, 0));
-  hipLaunchKernelGGL((k_mac<V>), dim3(blocks), dim3(256), 0, 0, out, 9u);
+  hipLaunchKernelGGL((k_mac<V>), dim3(blocks), dim3(threads), 0, 0, out, 9u);
   CHECK(hipEventRecord(e1, 0));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
-  const double macs = (double)blocks * 256 * ITERS * macs_per_iter;
-  printf("{\"variant\": \"%s\", \"blocks\": %d, \"ms\": %.4f, \"mad_Tops\": %.2f, \"frac_of_39.32\": %.3f}\n", name, blocks, ms,
-         macs / (ms * 1e-3) / 1e12, macs / (ms * 1e-3) / 1e12 / 39.32);
+  const double macs = (double)blocks * threads * ITERS * macs_per_iter;
+  const double waves = (double)blocks * ((threads + 63) / 64);
+  printf("{\"variant\": \"%s\", \"blocks\": %d, \"threads\": %d, \"ms\": %.4f, \"mad_Tops\": %.3f, \"frac_of_39.32\": %.3f, \"us_per_1k_mac_per_wave\": %.3f}\n", name, blocks, threads, ms,
+         macs / (ms * 1e-3) / 1e12, macs / (ms * 1e-3) / 1e12 / 39.32, 1e3 * ms / (ITERS * (double)macs_per_iter) * 1e3 * (waves > 0 ? 1.0 : 0.0));
 }
 
 int main(int argc, char** argv) {
   const int blocks = argc > 1 ? atoi(argv[1]) : 512;
+  const int threads = argc > 2 ? atoi(argv[2]) : 256;
+  const int only = argc > 3 ? atoi(argv[3]) : 0;
   uint64_t* out;
   CHECK(hipMalloc(&out, (size_t)blocks * 256 * 8));
-  run<0>("8 chains, conflict-free, one carry SGPR", out, blocks, 8);
-  run<1>("8 chains, bank conflicts", out, blocks, 8);
-  run<2>("8 chains, conflict-free, eight carry SGPRs", out, blocks, 8);
-  run<3>("16 chains, conflict-free", out, blocks, 16);
-  run<4>("4 chains, conflict-free", out, blocks, 8);
-  run<5>("1 chain", out, blocks, 8);
+  run<0>("8 chains, conflict-free, one carry SGPR", out, blocks, threads, 8);
+  if (only) return 0;
+  run<1>("8 chains, bank conflicts", out, blocks, threads, 8);
+  run<2>("8 chains, conflict-free, eight carry SGPRs", out, blocks, threads, 8);
+  run<3>("16 chains, conflict-free", out, blocks, threads, 16);
+  run<4>("4 chains, conflict-free", out, blocks, threads, 8);
+  run<5>("1 chain", out, blocks, threads, 8);
   return 0;
 }
