@@ -333,6 +333,30 @@ def count_fp_muls(pks, msgs, sigs, doms, strict=0, k=8):
     return {nm: tot[j] / done / ISSUED_MACS_PER_FP_MUL for j, nm in enumerate(names)}
 
 
+MAC_PROBE_FILE = os.path.join(ROOT, "profiles", "mac_probe_r05k.txt")
+
+
+def mac_stream_ceiling(achieved, peak):
+    """The rate a pure v_mad_u64_u32 stream reaches at the verify kernels' occupancy (two waves per
+    SIMD, tools/mac_probe.hip, measured once per build round): the ceiling any kernel at that occupancy
+    can approach, beside the issue-bound peak the frac is priced against."""
+    try:
+        rates = []
+        block = None
+        for ln in open(MAC_PROBE_FILE):
+            if ln.startswith("# blocks"):
+                block = int(ln.split()[-1])
+            elif ln.startswith("{") and block == 512:
+                rates.append(json.loads(ln)["mad_Tops"])
+        if not rates or not peak:
+            return None
+        top = max(rates)
+        return {"waves_per_simd": 2, "mac_only_Tops": top, "frac_of_peak": round(top / peak, 4),
+                "achieved_frac_of_ceiling": round(achieved / top, 4), "source": os.path.relpath(MAC_PROBE_FILE, ROOT)}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def agg_roofline(aprof, sample_pks, k, keys):
     """Roofline of the committee aggregation's dominant kernel: Fp multiplications per key of
     decode + add (the -DBLS_COUNT_OPS host build, hc_count_aggregate over one committee) x keys x
@@ -1077,6 +1101,7 @@ def main():
         roofline["pipeline_achieved"] = round(whole, 3)
         roofline["pipeline_frac"] = round(whole / peak, 4) if peak else None
         roofline["issue"] = issue_roofline(dom_kernels, n, kern_ms[dom_k])
+        roofline["occupancy_ceiling"] = mac_stream_ceiling(achieved, peak)
         line = {
             "metric": "BLS sig verifications/sec (whole node)",
             "value": round(value, 2),
