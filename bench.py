@@ -1002,6 +1002,18 @@ def main():
         elapsed = max(float(x.item()) for x in allt)
     total_items = n * args.steps * world
     value = total_items / elapsed
+    # the same K steps again with the per-launch HIP events off (the headline keeps
+    # the events, which the roofline's kernel times come from; this shows what they cost)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    quiet = _max_time(time.perf_counter() - t0, world, dist, dev)
+    counter[0] = 0
+    no_events = {"ms_per_step": round(1e3 * quiet / args.steps, 3), "value": round(total_items / quiet, 2)}
 
     def bench_other_policy():
         # the same batch under the other subgroup policy (same verdicts: no torsion points in it)
@@ -1122,6 +1134,7 @@ def main():
                        "batches_in_flight": kin,
                        "subgroup_policy": args.policy},
             "roofline": roofline,
+            "no_profiling_events": no_events,
         }
 
     # ---------------- secondary lines (other policy, C3 aggregation, deposits, randomized, C3-C5,
