@@ -813,6 +813,32 @@ def bench_native_comm(native, args, world, rank, dist, dev):
         t = _max_time(time.perf_counter() - t0, world, dist, dev)
         out["c4_aggregate"] = {"pubkeys": k, "pubkeys_aggregated_per_s": k * steps / t, "ms_per_aggregate": 1e3 * t / steps,
                                "note": "host keys in (PCIe copies inside the time), one collective call"}
+        # the same collective over device-resident keys: each rank's contiguous slice already in HBM
+        base, extra = divmod(k, world)
+        lo = rank * base + min(rank, extra)
+        cnt = base + (1 if rank < extra else 0)
+        d_keys = torch.from_numpy(np.ascontiguousarray(keys[lo:lo + cnt]).reshape(-1)).to(dev)
+        d_out = torch.zeros(48, dtype=torch.uint8, device=dev)
+        d_st = torch.zeros(1, dtype=torch.int32, device=dev)
+        d_ws = torch.empty(comm.aggregate_pubkeys_device_workspace_size(cnt), dtype=torch.uint8, device=dev)
+        cs = torch.cuda.current_stream(dev).cuda_stream
+
+        def dstep():
+            comm.aggregate_pubkeys_device(cnt, d_keys.data_ptr(), d_out.data_ptr(), d_st.data_ptr(), d_ws.data_ptr(), cs)
+        dstep()
+        torch.cuda.synchronize()
+        assert bytes(d_out.cpu().numpy()) == want and int(d_st.item()) == 0, "native C4 device aggregate mismatch"
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            dstep()
+        torch.cuda.synchronize()
+        t = _max_time(time.perf_counter() - t0, world, dist, dev)
+        out["c4_aggregate_device"] = {"pubkeys": k, "pubkeys_aggregated_per_s": k * steps / t,
+                                      "ms_per_aggregate": 1e3 * t / steps,
+                                      "note": "device-resident keys (each rank its slice), result in HBM on every rank"}
         rng = np.random.default_rng(0xB15_0005)
         Lm = 4096
         sks = [int.from_bytes(rng.bytes(32), "big") % (R_ORDER - 1) + 1 for _ in range(Lm)]

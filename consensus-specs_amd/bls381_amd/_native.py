@@ -82,6 +82,8 @@ _SIGS = {
     "bls381_comm_destroy": (None, []),
     "bls381_verify_multiple_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]),
     "bls381_aggregate_pubkeys_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p]),
+    "bls381_aggregate_pubkeys_sharded_device_workspace_size": (ctypes.c_size_t, [ctypes.c_size_t]),
+    "bls381_aggregate_pubkeys_sharded_device": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, _u8p, _u8p]),
     "bls381_verify_multiple_batch_sharded": (ctypes.c_int, [ctypes.c_size_t, _u8p, _u8p, _u8p, ctypes.c_size_t,
                                                             _u8p, _u8p, _u8p]),
     "bls381_ssz_root_batch": (ctypes.c_int, [ctypes.c_size_t, _u8p, ctypes.c_size_t, _u8p, ctypes.c_uint32, _u8p]),

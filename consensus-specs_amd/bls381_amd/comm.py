@@ -154,6 +154,20 @@ def aggregate_pubkeys(pubkeys: Sequence[bytes]) -> bytes:
     return out.raw
 
 
+def aggregate_pubkeys_device_workspace_size(n_local: int) -> int:
+    return int(_native.lib().bls381_aggregate_pubkeys_sharded_device_workspace_size(n_local))
+
+
+def aggregate_pubkeys_device(n_local: int, d_pks: int, d_out48: int, d_status: int, d_workspace: int,
+                             stream: int = 0) -> None:
+    """Collective bls_aggregate_pubkeys over device-resident keys (device pointers as ints): this
+    rank's n_local keys in, the aggregate (48 B) and the status (int32, 0 or EINVAL_POINT) out on every
+    rank, queued on `stream`; no host copy, no synchronisation."""
+    _native.check(_native.lib().bls381_aggregate_pubkeys_sharded_device(
+        n_local, ctypes.c_void_p(d_pks), ctypes.c_void_p(d_out48), ctypes.c_void_p(d_status),
+        ctypes.c_void_p(d_workspace), ctypes.c_void_p(stream)))
+
+
 def verify_multiple_batch(call_off, pks: bytes, msgs: bytes, msg_len: int, sigs: bytes, dom8s: bytes) -> List[bool]:
     """Independent calls over the ranks (same arguments on every rank); all verdicts on every rank."""
     call_off = np.ascontiguousarray(call_off, dtype=np.uint32)

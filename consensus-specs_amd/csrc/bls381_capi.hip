@@ -372,6 +372,20 @@ int launch_hash_g2(hipStream_t s, size_t n, const uint8_t* msgs, uint32_t mlen, 
          (const uint32_t*)nullptr, prio);
   return 0;
 }
+// hash_to_G2 with the search offsets known (koff from k_hash_search, or nullptr): the latency
+// batches.  BLS381_HASH_QUAD_MAX_N (default 8192, 0 = off): up to that many messages the cofactor
+// map runs on lane quads (k_hash_g2_q), its independent products two at a time.
+int launch_hash_koff(hipStream_t s, size_t n, const uint8_t* msgs, uint32_t mlen, const uint8_t* doms, int dom_stride,
+                     uint32_t* h_aff, uint8_t* st, const uint32_t* koff, int prio) {
+  static const size_t quad_max = (size_t)env_knob("BLS381_HASH_QUAD_MAX_N", 8192);
+  if (n <= quad_max)
+    LAUNCH("hash_to_g2_q", s, dim3(grid_for(4 * n)), dim3(KBLOCK), k_hash_g2_q, n, msgs, mlen, doms, dom_stride, h_aff,
+           st, koff, prio);
+  else
+    LAUNCH("hash_to_g2", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_hash_g2, n, msgs, mlen, doms, dom_stride, h_aff,
+           st, koff, prio);
+  return 0;
+}
 #define LAUNCH_HASH(...)                        \
   do {                                          \
     int rc__ = launch_hash_g2(__VA_ARGS__);     \
@@ -449,9 +463,8 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
     LAUNCH("hash_bp", s, g2, b, k_hash_bp, n, w.h_aff, (uint8_t*)nullptr);
   } else if (!wide)
     LAUNCH_HASH(s, n, msgs, 32u, doms, 8, w.h_aff, (uint8_t*)nullptr);
-  else
-    LAUNCH("hash_to_g2", s, g2, b, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr,
-           (const uint32_t*)w.koff, 0);
+  else if (int rc_h = launch_hash_koff(s, n, msgs, 32u, doms, 8, w.h_aff, (uint8_t*)nullptr, (const uint32_t*)w.koff, 0))
+    return rc_h;
   HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
 #if BLS_DECODE_G2_SIDE
   if (c2_order == 4 && (g2_one_lane() & 1)) HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -1136,10 +1149,9 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
                (uint32_t)mlen, (const uint8_t*)d_gdom, 8, d_koff);
       if (!wide && !pl.tasks)
         LAUNCH_HASH(s, G, (const uint8_t*)d_gmsg, (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st);
-      else
-        LAUNCH("hash_to_g2", s, dim3(grid_for(2 * G)), dim3(KBLOCK), k_hash_g2, G, (const uint8_t*)d_gmsg,
-               (uint32_t)mlen, (const uint8_t*)d_gdom, 8, h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr),
-               pl.tasks ? 1 : 0);
+      else if (int rc_h = launch_hash_koff(s, G, (const uint8_t*)d_gmsg, (uint32_t)mlen, (const uint8_t*)d_gdom, 8,
+                                           h_aff, h_st, (const uint32_t*)(wide ? d_koff : nullptr), pl.tasks ? 1 : 0))
+        return rc_h;
     }
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -2311,6 +2323,9 @@ struct Comm {
   int nranks = 0, rank = -1, device = -1;
   uint8_t* rows = nullptr;   // gathered per-rank rows (device), grown on demand
   size_t rows_cap = 0;
+  // the device-resident collectives leave their work queued on the caller's stream: the next
+  // call that reuses `rows` waits for it (created with the communicator)
+  hipEvent_t rows_ev = nullptr;
 };
 std::mutex g_comm_mu;
 Comm g_comm;
@@ -2390,6 +2405,7 @@ int comm_rows(Comm* cm, size_t bytes, uint8_t** out) {
 int comm_alloc_rows(Comm* cm) {
   HIPC(hipMalloc(&cm->rows, COMM_ROWS_BYTES));
   cm->rows_cap = COMM_ROWS_BYTES;
+  if (!cm->rows_ev) HIPC(hipEventCreateWithFlags(&cm->rows_ev, hipEventDisableTiming));
   return 0;
 }
 
@@ -2449,7 +2465,11 @@ int bls381_comm_init(int nranks, int rank, const uint8_t uid[128]) {
   std::memcpy(&id, uid, sizeof(id));
   ncclComm_t comm;
   ncclResult_t nr = api->comm_init_rank(&comm, nranks, id, rank);
-  if (nr != ncclSuccess) { (void)hipFree(fresh.rows); return nccl_fail(api, "ncclCommInitRank", nr); }
+  if (nr != ncclSuccess) {
+    (void)hipFree(fresh.rows);
+    if (fresh.rows_ev) (void)hipEventDestroy(fresh.rows_ev);
+    return nccl_fail(api, "ncclCommInitRank", nr);
+  }
   g_comm = fresh;
   g_comm.comm = comm;
   g_comm.nranks = nranks;
@@ -2495,6 +2515,7 @@ void bls381_comm_destroy(void) {
     (void)hipDeviceSynchronize();
     (void)hipFree(g_comm.rows);
   }
+  if (g_comm.rows_ev) (void)hipEventDestroy(g_comm.rows_ev);
   g_comm = Comm();
 }
 
@@ -2520,6 +2541,7 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
   hipStream_t s = c->stream;
   uint8_t* d_rows;
   if ((rc = comm_rows(cm, 576 * R + 576 + 64, &d_rows))) return rc;   // fits by construction (init)
+  if (cm->rows_ev) (void)hipEventSynchronize(cm->rows_ev);   // a device-form call may still use them
   uint8_t* d_v = d_rows + 576 * R + 576;
   // local stage: this rank's row(s); on failure the row is zero (verdict False on rank 0)
   int local = local_stage([&]() -> int {
@@ -2617,6 +2639,7 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
   hipStream_t s = c->stream;
   uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
   if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;   // fits by construction (init)
+  if (cm->rows_ev) (void)hipEventSynchronize(cm->rows_ev);   // a device-form call may still use them
   uint8_t* d_sum = d_rows + 48 * R + 48;
   int32_t* d_st = (int32_t*)(d_sum + 64);
   // contiguous ranges, sizes differing by at most one (sharding.shard_range)
@@ -2678,6 +2701,87 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
   return local ? local : st;
 }
 
+// Device-resident form of bls381_aggregate_pubkeys_sharded (include/bls381.h): this rank's keys
+// are already in HBM and every rank receives the aggregate and the status in HBM, on the caller's
+// stream; the call returns with its work queued (no host copy, no synchronisation).  Same protocol:
+// this rank's partial (compressed, 48 zero bytes on an error), all-gathered, decoded and summed on
+// rank 0 with the strict codec, broadcast.
+static constexpr size_t SHARDED_MAX_RANKS = 4096;
+
+size_t bls381_aggregate_pubkeys_sharded_device_workspace_size(size_t n_local) {
+  return bls381_aggregate_pubkeys_batch_workspace_size(1, n_local) +
+         bls381_aggregate_pubkeys_batch_workspace_size(1, SHARDED_MAX_RANKS);
+}
+
+int bls381_aggregate_pubkeys_sharded_device(size_t n_local, const uint8_t* d_pks, uint8_t* d_out48,
+                                            int32_t* d_status, void* d_workspace, void* stream) {
+  if (!d_out48 || !d_status || !d_workspace || (n_local && !d_pks)) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> clk(g_comm_mu);
+  Comm* cm = comm_ctx(&rc);
+  if (!cm) return rc;
+  RcclApi* api = cm->virt ? nullptr : rccl_api();
+  if (!cm->virt && !api) return BLS381_ENODEV;
+  const size_t R = (size_t)cm->nranks;
+  if (R > SHARDED_MAX_RANKS) { t_err = "too many ranks for the device form"; return BLS381_EARG; }
+  hipStream_t s = (hipStream_t)stream;
+  uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
+  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;
+  uint8_t* d_sum = d_rows + 48 * R + 48;
+  int32_t* d_st = (int32_t*)(d_sum + 64);
+  if (cm->rows_ev) (void)hipStreamWaitEvent(s, cm->rows_ev, 0);   // before any collective: no early return
+  const size_t ws_local = bls381_aggregate_pubkeys_batch_workspace_size(1, n_local);
+  uint8_t* ws_root = (uint8_t*)d_workspace + ws_local;
+  const size_t ws_root_cap = bls381_aggregate_pubkeys_batch_workspace_size(1, SHARDED_MAX_RANKS);
+  // virtual: one process plays every rank over the whole call, split as the host form splits it
+  const size_t base = n_local / R, extra = n_local % R;
+  int local = 0;
+  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
+    const size_t rr = (size_t)r;
+    uint8_t* part = cm->virt ? d_rows + 48 * rr : d_rows + 48 * R;
+    const size_t lo = cm->virt ? rr * base + (rr < extra ? rr : extra) : 0;
+    const size_t cnt = cm->virt ? base + (rr < extra ? 1 : 0) : n_local;
+    const int lrc = local_stage([&]() -> int {
+      const uint32_t off1[2] = {0, (uint32_t)cnt};
+      int e;
+      // the ranks of a virtual communicator reuse the workspace in stream order
+      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks + 48 * lo, part, d_st, d_workspace, ws_local, s,
+                              policy_flags(0))))
+        return e;
+      LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
+      return 0;
+    });
+    if (lrc) {
+      (void)hipMemsetAsync(part, 0, 48, s);   // 48 zero bytes: not an encoding, the sum is flagged
+      if (!local) local = lrc;
+    }
+  }
+  if (local && cm->virt) return local;
+  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 48 * R, d_rows, 48, ncclUint8, cm->comm, s));
+  if (is_root(cm)) {
+    const int root = local_stage([&]() -> int {
+      const uint32_t offR[2] = {0, (uint32_t)R};
+      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, ws_root, ws_root_cap, s, 0);
+    });
+    if (root) {
+      static const int32_t err = BLS381_EHIP;   // a copy source that outlives the queued copy
+      (void)hipMemsetAsync(d_sum, 0, 48, s);
+      (void)hipMemcpyAsync(d_st + 1, &err, 4, hipMemcpyHostToDevice, s);
+      if (!local) local = root;
+    }
+  }
+  if (!cm->virt) {
+    NCCLC(api, api->broadcast(d_sum, d_sum, 48, ncclUint8, 0, cm->comm, s));
+    NCCLC(api, api->broadcast(d_st + 1, d_st + 1, 4, ncclUint8, 0, cm->comm, s));
+  }
+  HIPC(hipMemcpyAsync(d_out48, d_sum, 48, hipMemcpyDeviceToDevice, s));
+  HIPC(hipMemcpyAsync(d_status, d_st + 1, 4, hipMemcpyDeviceToDevice, s));
+  if (cm->rows_ev) HIPC(hipEventRecord(cm->rows_ev, s));
+  return local;
+}
+
 int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
                                          const uint8_t* msgs, size_t msg_len, const uint8_t* sigs,
                                          const uint8_t* dom8s, uint8_t* verdicts) {
@@ -2719,6 +2823,7 @@ int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_of
     uint8_t* d_rows;
     const size_t piece = std::min(width, COMM_ROWS_BYTES / (R + 1));
     if ((rc = comm_rows(cm, piece * (R + 1), &d_rows))) return rc;   // fits by construction
+    if (cm->rows_ev) (void)hipEventSynchronize(cm->rows_ev);   // a device-form call may still use them
     // every rank issues the same all-gathers (width and piece are the same everywhere) even after
     // an error of its own, so no peer waits on a collective this rank skipped
     int err = 0;

@@ -208,6 +208,131 @@ __device__ __forceinline__ void line_dbl_q1(g2_proj<fp2p_t>& T, const g1_line_pr
   T.z = fp2_dbl(qd_sel(hi, m2, m2o));
 }
 
+// ------------------------------------------- G2 point arithmetic on a quad --
+// The latency form of hash_to_G2's cofactor map (k_hash_g2_q): the running point is held on both
+// halves and the independent products of each step run on the two halves at once, as in
+// line_dbl_q1.  Every value is the same on both halves after each step, so the exceptional-case
+// branches of the point formulas stay uniform within the quad.  The same formulas as
+// bls381_curve.hpp (dbl-2009-l, add-2007-bl, mixed addition); a square paired with a product runs
+// as a product of the value with itself (the same field element; representations < 2q).
+//   jac_dbl 7 products -> 4 steps, jac_add_aff 11 -> 6, jac_add 16 -> 8, psi 2 -> 1.
+// lo's value and hi's value of a split step, on both halves
+__device__ __forceinline__ void qd_both(const fp2p_t& mine, fp2p_t& lo_v, fp2p_t& hi_v) {
+  const bool hi = qd_hi();
+  const fp2p_t o = qd_swap(mine);
+  lo_v = qd_sel(hi, o, mine);
+  hi_v = qd_sel(hi, mine, o);
+}
+
+__device__ __forceinline__ jac_t<fp2p_t> jac_dbl_q(const jac_t<fp2p_t>& p) {
+  const bool hi = qd_hi();
+  fp2p_t A, B, C, XB2, Fv, YZ;
+  qd_both(fp2_sqr(qd_sel(hi, p.y, p.x)), A, B);                                   // X^2 | Y^2
+  qd_both(fp2_sqr(qd_sel(hi, fp2_add(p.x, B), B)), C, XB2);                       // B^2 | (X + B)^2
+  const fp2p_t D = fp2_dbl(fp2_sub2(XB2, A, C));
+  const fp2p_t E = fp2_mul_small(A, 3);
+  qd_both(fp2_mul(qd_sel(hi, p.y, E), qd_sel(hi, p.z, E)), Fv, YZ);              // E^2 | Y Z
+  jac_t<fp2p_t> r;
+  r.x = fp2_sub2(Fv, D, D);
+  r.y = fp2_sub(fp2_mul(E, fp2_sub(D, r.x)), fp2_mul_small(C, 8));
+  r.z = fp2_dbl(YZ);
+  return r;   // Z = 0 stays 0
+}
+
+__device__ __forceinline__ jac_t<fp2p_t> jac_add_aff_q(const jac_t<fp2p_t>& p, const aff_t<fp2p_t>& q) {
+  if (jac_is_inf(p)) return jac_from_aff(q);
+  const bool hi = qd_hi();
+  fp2p_t Z1Z1, Y2Z1, U2, S2;
+  qd_both(fp2_mul(p.z, qd_sel(hi, q.y, p.z)), Z1Z1, Y2Z1);                       // Z1^2 | y2 Z1
+  qd_both(fp2_mul(Z1Z1, qd_sel(hi, Y2Z1, q.x)), U2, S2);                         // x2 Z1Z1 | y2 Z1 Z1Z1
+  const fp2p_t H = fp2_sub(U2, p.x);
+  const fp2p_t R = fp2_sub(S2, p.y);
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(R)) return jac_dbl_q(p);
+    return jac_infinity<fp2p_t>();
+  }
+  fp2p_t HH, Z3, HHH, V, RR, YH;
+  qd_both(fp2_mul(H, qd_sel(hi, p.z, H)), HH, Z3);                               // H^2 | Z1 H
+  qd_both(fp2_mul(HH, qd_sel(hi, p.x, H)), HHH, V);                              // H HH | X1 HH
+  qd_both(fp2_mul(qd_sel(hi, p.y, R), qd_sel(hi, HHH, R)), RR, YH);              // R^2 | Y1 HHH
+  jac_t<fp2p_t> r;
+  r.x = fp2_sub2(RR, HHH, fp2_dbl(V));
+  r.y = fp2_sub(fp2_mul(R, fp2_sub(V, r.x)), YH);
+  r.z = Z3;
+  return r;
+}
+
+__device__ __forceinline__ jac_t<fp2p_t> jac_add_q(const jac_t<fp2p_t>& p, const jac_t<fp2p_t>& q) {
+  if (jac_is_inf(p)) return q;
+  if (jac_is_inf(q)) return p;
+  const bool hi = qd_hi();
+  fp2p_t Z1Z1, Z2Z2, U1, U2, Y1Z2, Y2Z1, S1, S2;
+  qd_both(fp2_sqr(qd_sel(hi, q.z, p.z)), Z1Z1, Z2Z2);                            // Z1^2 | Z2^2
+  qd_both(fp2_mul(qd_sel(hi, q.x, p.x), qd_sel(hi, Z1Z1, Z2Z2)), U1, U2);       // X1 Z2Z2 | X2 Z1Z1
+  qd_both(fp2_mul(qd_sel(hi, q.y, p.y), qd_sel(hi, p.z, q.z)), Y1Z2, Y2Z1);     // Y1 Z2 | Y2 Z1
+  qd_both(fp2_mul(qd_sel(hi, Y2Z1, Y1Z2), qd_sel(hi, Z1Z1, Z2Z2)), S1, S2);     // Y1 Z2 Z2Z2 | Y2 Z1 Z1Z1
+  const fp2p_t H = fp2_sub(U2, U1);
+  const fp2p_t R = fp2_sub(S2, S1);
+  if (fp2_is_zero(H)) {
+    if (fp2_is_zero(R)) return jac_dbl_q(p);
+    return jac_infinity<fp2p_t>();
+  }
+  fp2p_t HH, Z1Z2, HHH, V, RR, SH;
+  qd_both(fp2_mul(qd_sel(hi, p.z, H), qd_sel(hi, q.z, H)), HH, Z1Z2);           // H^2 | Z1 Z2
+  qd_both(fp2_mul(HH, qd_sel(hi, U1, H)), HHH, V);                               // H HH | U1 HH
+  qd_both(fp2_mul(qd_sel(hi, S1, R), qd_sel(hi, HHH, R)), RR, SH);               // R^2 | S1 HHH
+  jac_t<fp2p_t> r;
+  r.x = fp2_sub2(RR, HHH, fp2_dbl(V));
+  fp2p_t RV, Z3;
+  qd_both(fp2_mul(qd_sel(hi, Z1Z2, R), qd_sel(hi, H, fp2_sub(V, r.x))), RV, Z3); // R (V - X3) | Z1 Z2 H
+  r.y = fp2_sub(RV, SH);
+  r.z = Z3;
+  return r;
+}
+
+// psi on Jacobian coordinates: (cx conj(X), cy conj(Y), conj(Z)), the two products at once
+__device__ __forceinline__ jac_t<fp2p_t> g2_psi_jac_q(const jac_t<fp2p_t>& p) {
+  const bool hi = qd_hi();
+  jac_t<fp2p_t> r;
+  const fp2p_t k = qd_sel(hi, e2_k<fp2p_t>(PSI_CY_M), e2_k<fp2p_t>(PSI_CX_M));
+  qd_both(fp2_mul(k, fp2_conj(qd_sel(hi, p.y, p.x))), r.x, r.y);
+  r.z = fp2_conj(p.z);
+  return r;
+}
+
+// [k] a (affine base) and [k] p (Jacobian base) for a 64-bit k, left to right
+__device__ __noinline__ jac_t<fp2p_t> jac_mul_u64_q(const aff_t<fp2p_t> a, uint64_t k) {
+  jac_t<fp2p_t> r = jac_from_aff(a);
+  int top = 63;
+  while (top > 0 && !((k >> top) & 1)) --top;
+  for (int i = top - 1; i >= 0; --i) {
+    r = jac_dbl_q(r);
+    if ((k >> i) & 1) r = jac_add_aff_q(r, a);
+  }
+  return r;
+}
+__device__ __noinline__ jac_t<fp2p_t> jac_mul_u64_jac_q(const jac_t<fp2p_t> p, uint64_t k) {
+  jac_t<fp2p_t> r = p;
+  int top = 63;
+  while (top > 0 && !((k >> top) & 1)) --top;
+  for (int i = top - 1; i >= 0; --i) {
+    r = jac_dbl_q(r);
+    if ((k >> i) & 1) r = jac_add_q(r, p);
+  }
+  return r;
+}
+
+// g2_mul_bp (bls381_hash.hpp) on a quad: BP(P) = [x^2 - x - 1]P + [x - 1]psi(P) + 2 psi^2(P)
+__device__ __noinline__ jac_t<fp2p_t> g2_mul_bp_q(const aff_t<fp2p_t> p) {
+  aff_t<fp2p_t> np;
+  np.x = p.x;
+  np.y = fp2_neg(p.y);
+  const jac_t<fp2p_t> t1 = jac_mul_u64_q(p, BLS_X_ABS);                                   // [|x|]P
+  jac_t<fp2p_t> Q0 = jac_add_aff_q(jac_add_q(jac_mul_u64_jac_q(t1, BLS_X_ABS), t1), np);  // [x^2 - x - 1]P
+  Q0 = jac_add_q(Q0, g2_psi_jac_q(jac_add_aff_q(jac_neg(t1), np)));                      // + psi([x - 1]P)
+  return jac_add_q(Q0, g2_psi_jac_q(g2_psi_jac_q(jac_dbl_q(jac_from_aff(p)))));          // + psi^2(2P)
+}
+
 // line_add with its products split (lo | hi per step)
 __device__ __forceinline__ void line_add_q1(g2_proj<fp2p_t>& T, const aff_t<fp2p_t>& Q, const g1_line_pre& P,
                                             fp2p_t& c0, fp2p_t& c1, fp2p_t& c2) {

@@ -254,6 +254,15 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
  * partials all-gathered and summed on rank 0, broadcast.  Returns 0 or
  * BLS381_EINVAL_POINT (any rank's invalid encoding) on every rank. */
 int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]);
+/* Device-resident form: this rank's n_local keys (its contiguous range of the call, in rank
+ * order; a virtual communicator takes the whole call) are already in HBM at d_pks; every rank
+ * receives the aggregate in d_out48 and the status (0 or BLS381_EINVAL_POINT) in d_status[0],
+ * queued on `stream` with no host copy and no synchronisation.  Replaces the host-buffer form's
+ * PCIe copies for callers whose keys are device-resident (bls.py:34-36 aggregate_pubkeys,
+ * SURVEY.md §8e).  Returns 0 or a launch / RCCL error code. */
+size_t bls381_aggregate_pubkeys_sharded_device_workspace_size(size_t n_local);
+int bls381_aggregate_pubkeys_sharded_device(size_t n_local, const uint8_t* d_pks, uint8_t* d_out48,
+                                            int32_t* d_status, void* d_workspace, void* stream);
 /* Independent verify_multiple calls, contiguous call ranges per rank (a call's
  * final exponentiation is never split); every rank receives all verdicts. */
 int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,

@@ -1095,6 +1095,24 @@ def _comm_checks(native, golden, torsion, noncanon):
         sum((i % 40) + 1 for i in range(1000)))
     with pytest.raises(ValueError):
         comm.aggregate_pubkeys(keys[:7] + [h(gb["invalid_g1"][1])])
+    # the device-resident form (one process holds the whole call: world 1, or every virtual rank)
+    import torch
+
+    def dev_agg(pk_list):
+        blob = b"".join(pk_list)
+        d_pks = torch.frombuffer(bytearray(blob + b"\0"), dtype=torch.uint8)[:len(blob)].cuda()
+        d_out = torch.zeros(48, dtype=torch.uint8, device="cuda")
+        d_st = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+        d_ws = torch.empty(comm.aggregate_pubkeys_device_workspace_size(len(pk_list)), dtype=torch.uint8, device="cuda")
+        s = torch.cuda.current_stream()
+        comm.aggregate_pubkeys_device(len(pk_list), d_pks.data_ptr(), d_out.data_ptr(), d_st.data_ptr(),
+                                      d_ws.data_ptr(), s.cuda_stream)
+        torch.cuda.synchronize()
+        return bytes(d_out.cpu().numpy()), int(d_st.item())
+    for c in gb["aggregate_pubkeys"] + torsion["aggregate_pubkeys"]:
+        assert dev_agg([h(p) for p in c["input"]]) == (bytes.fromhex(c["output"]), 0), c["kind"]
+    assert dev_agg([keys[i % 40] for i in range(1000)]) == (O.privtopub(sum((i % 40) + 1 for i in range(1000))), 0)
+    assert dev_agg(keys[:7] + [h(gb["invalid_g1"][1])])[1] == native.EINVAL_POINT
     off, pks, msgs, sigs, doms = [0], b"", b"", b"", b""
     for c, _ in vms * 2:
         pks += b"".join(h(p) for p in c["pubkeys"]); msgs += b"".join(h(m) for m in c["messages"])
