@@ -2624,93 +2624,136 @@ int bls381_verify_multiple_sharded(size_t n, const uint8_t* pks, const uint8_t* 
   return v ? 1 : 0;
 }
 
-int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]) {
-  if (!out || (n && !pks)) return BLS381_EARG;
+// The device form's per-rank row: the partial sum as a Jacobian point (x, y, z: 3 x 14 Montgomery
+// words) and a bad flag (any member failed to decode), 44 words.  Rank 0 sums the rows without
+// decompressing anything (the host form ships compressed partials and decodes them: one Fp square
+// root per rank on rank 0's critical path).
+constexpr size_t AGG_ROW_WORDS = 44;
+__global__ void __launch_bounds__(64) k_agg_jac_row(const uint32_t* __restrict__ jac, const uint8_t* __restrict__ bad,
+                                                   uint32_t* __restrict__ row) {
+  const uint32_t t = threadIdx.x;
+  if (t < 42) row[t] = jac[t];   // SoA of one group: the 42 words in (coordinate, limb) order
+  if (t == 42) row[42] = bad[0] ? 1u : 0u;
+  if (t == 43) row[43] = 0;
+}
+// one wave: lane j sums rows j, j + 64, ...; an LDS tree combines the 64 partial sums; lane 0
+// compresses the total (or flags it, when any rank's row is bad)
+__global__ void __launch_bounds__(64) k_agg_sum_rows(uint32_t R, const uint32_t* __restrict__ rows,
+                                                    uint8_t* __restrict__ out48, int32_t* __restrict__ status) {
+  __shared__ uint32_t part[64][42];
+  __shared__ uint32_t anybad;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) anybad = 0;
+  __syncthreads();
+  jac_t<fp_t> acc = jac_infinity<fp_t>();
+  uint32_t bad = 0;
+  for (uint32_t r = t; r < R; r += 64) {
+    const uint32_t* row = rows + (size_t)r * AGG_ROW_WORDS;
+    jac_t<fp_t> p;
+#pragma unroll
+    for (int k = 0; k < FP_LIMBS; ++k) { p.x.w[k] = row[k]; p.y.w[k] = row[14 + k]; p.z.w[k] = row[28 + k]; }
+    bad |= row[42];
+    acc = jac_add(acc, p);
+  }
+  if (bad) atomicOr(&anybad, 1u);
+  auto put = [&](const jac_t<fp_t>& a) {
+#pragma unroll
+    for (int k = 0; k < FP_LIMBS; ++k) { part[t][k] = a.x.w[k]; part[t][14 + k] = a.y.w[k]; part[t][28 + k] = a.z.w[k]; }
+  };
+  auto get = [&](uint32_t j) {
+    jac_t<fp_t> a;
+#pragma unroll
+    for (int k = 0; k < FP_LIMBS; ++k) { a.x.w[k] = part[j][k]; a.y.w[k] = part[j][14 + k]; a.z.w[k] = part[j][28 + k]; }
+    return a;
+  };
+  put(acc);
+  __syncthreads();
+  for (uint32_t w = 32; w >= 1; w >>= 1) {
+    if (t < w) put(jac_add(get(t), get(t + w)));
+    __syncthreads();
+  }
+  if (t != 0) return;
+  if (anybad) {
+    for (int b = 0; b < 48; ++b) out48[b] = 0;
+    *status = BLS381_EINVAL_POINT;
+    return;
+  }
+  pt_compress(out48, get(0));
+  *status = 0;
+}
+
+// Device-resident form of bls381_aggregate_pubkeys_sharded (include/bls381.h): this rank's keys
+// are already in HBM and every rank receives the aggregate and the status in HBM, on the caller's
+// stream; the call returns with its work queued (no host copy, no synchronisation).  This rank's
+// partial sum travels as a Jacobian row (k_agg_jac_row), the rows are all-gathered and rank 0 sums
+// them (k_agg_sum_rows) and compresses once; the aggregate and status are broadcast.
+size_t bls381_aggregate_pubkeys_sharded_device_workspace_size(size_t n_local) {
+  return bls381_aggregate_pubkeys_batch_workspace_size(1, n_local);
+}
+
+// the protocol with g_comm_mu held: this rank's n_local keys at d_pks (a virtual communicator: the
+// whole call), aggregate and status into device memory, all on stream s
+static int agg_sharded_impl(Ctx* c, Comm* cm, RcclApi* api, size_t n_local, const uint8_t* d_pks, uint8_t* d_out48,
+                            int32_t* d_status, void* d_workspace, hipStream_t s, int force_err = 0) {
   int rc = 0;
-  Ctx* c = get_ctx(&rc);
-  if (!c) return rc;
-  std::lock_guard<std::mutex> clk(g_comm_mu);
-  Comm* cm = comm_ctx(&rc);
-  if (!cm) return rc;
-  RcclApi* api = cm->virt ? nullptr : rccl_api();
-  if (!cm->virt && !api) return BLS381_ENODEV;
   const size_t R = (size_t)cm->nranks;
-  std::lock_guard<std::mutex> lk(c->mu);
-  hipStream_t s = c->stream;
-  uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
-  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;   // fits by construction (init)
-  if (cm->rows_ev) (void)hipEventSynchronize(cm->rows_ev);   // a device-form call may still use them
-  uint8_t* d_sum = d_rows + 48 * R + 48;
+  const size_t row_b = 4 * AGG_ROW_WORDS;
+  uint8_t* d_rows;   // R rows, then this rank's own, then the sum (48 B) and the status
+  if ((rc = comm_rows(cm, row_b * (R + 1) + 64 + 64, &d_rows))) return rc;   // fits by construction (init)
+  uint8_t* d_sum = d_rows + row_b * (R + 1);
   int32_t* d_st = (int32_t*)(d_sum + 64);
-  // contiguous ranges, sizes differing by at most one (sharding.shard_range)
-  const size_t base = n / R, extra = n % R;
+  if (cm->rows_ev) (void)hipStreamWaitEvent(s, cm->rows_ev, 0);   // before any collective: no early return
+  const size_t ws_local = bls381_aggregate_pubkeys_sharded_device_workspace_size(n_local);
+  // virtual: one process plays every rank over the whole call, split as the host form splits it
+  const size_t base = n_local / R, extra = n_local % R;
   int local = 0;
   for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
     const size_t rr = (size_t)r;
-    uint8_t* part = cm->virt ? d_rows + 48 * rr : d_rows + 48 * R;
-    const int lrc = local_stage([&]() -> int {
-      const size_t lo = rr * base + (rr < extra ? rr : extra), cnt = base + (rr < extra ? 1 : 0);
+    uint32_t* row = (uint32_t*)(cm->virt ? d_rows + row_b * rr : d_rows + row_b * R);
+    const size_t lo = cm->virt ? rr * base + (rr < extra ? rr : extra) : 0;
+    const size_t cnt = cm->virt ? base + (rr < extra ? 1 : 0) : n_local;
+    const int lrc = force_err ? force_err : local_stage([&]() -> int {
       const uint32_t off1[2] = {0, (uint32_t)cnt};
-      const size_t ws1 = agg_ws_bytes(0, 1, off1);
+      auto hold = std::make_shared<AggPlan>(plan_agg(1, off1, 1));
+      const uint32_t* jac;
+      const uint8_t* bad;
+      size_t used = 0;
       int e;
-      if ((e = ensure_ws(c, align256(48 * cnt + 1) + ws1 + 8192))) return e;
-      Bump b(c->ws, c->ws_cap);
-      uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
-      void* w1 = b.take<uint8_t>(ws1);
-      if (cnt) HIPC(hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s));
-      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks, part, d_st, w1, ws1, s, policy_flags(0)))) return e;
-      // an invalid encoding anywhere: this partial becomes 48 zero bytes, itself invalid
-      LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
-      HIPC(hipStreamSynchronize(s));   // the host slice and the workspace are reused
-      return 0;
+      // the ranks of a virtual communicator reuse the workspace in stream order
+      if ((e = run_agg<fp_t>(*hold, 1, d_pks + 48 * lo, d_workspace, s, &jac, &bad, &used, ws_local, nullptr,
+                             policy_flags(0))))
+        return e;
+      LAUNCH("agg_jac_row", s, dim3(1), dim3(64), k_agg_jac_row, jac, bad, row);
+      return keep_until_done(c, s, hold);
     });
     if (lrc) {
-      (void)hipStreamSynchronize(s);
-      (void)hipMemsetAsync(part, 0, 48, s);   // 48 zero bytes: not an encoding, the sum is flagged
+      (void)hipMemsetAsync(row, 0, row_b, s);                   // z = 0 and the bad flag set:
+      (void)hipMemsetAsync((uint8_t*)row + 4 * 42, 1, 1, s);   // the sum is flagged
       if (!local) local = lrc;
     }
   }
   if (local && cm->virt) return local;
-  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 48 * R, d_rows, 48, ncclUint8, cm->comm, s));
-  if (is_root(cm)) {   // the partials are compressed points: decode + sum them on rank 0
+  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + row_b * R, d_rows, row_b, ncclUint8, cm->comm, s));
+  if (is_root(cm)) {
     const int root = local_stage([&]() -> int {
-      const uint32_t offR[2] = {0, (uint32_t)R};
-      const size_t wsR = agg_ws_bytes(0, 1, offR);
-      int e;
-      if ((e = ensure_ws(c, wsR + 4096))) return e;
-      // strict codec: the partials are this library's own canonical encodings, and a zero row
-      // (an error on its rank) must stay invalid -- the lax codec would decode it to (0, 2)
-      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, c->ws, c->ws_cap, s, 0);
+      LAUNCH("agg_sum_rows", s, dim3(1), dim3(64), k_agg_sum_rows, (uint32_t)R, (const uint32_t*)d_rows, d_sum, d_st);
+      return 0;
     });
     if (root) {
-      (void)hipStreamSynchronize(s);
       static const int32_t err = BLS381_EHIP;   // a copy source that outlives the queued copy
       (void)hipMemsetAsync(d_sum, 0, 48, s);
-      (void)hipMemcpyAsync(d_st + 1, &err, 4, hipMemcpyHostToDevice, s);
+      (void)hipMemcpyAsync(d_st, &err, 4, hipMemcpyHostToDevice, s);
       if (!local) local = root;
     }
   }
   if (!cm->virt) {
     NCCLC(api, api->broadcast(d_sum, d_sum, 48, ncclUint8, 0, cm->comm, s));
-    NCCLC(api, api->broadcast(d_st + 1, d_st + 1, 4, ncclUint8, 0, cm->comm, s));
+    NCCLC(api, api->broadcast(d_st, d_st, 4, ncclUint8, 0, cm->comm, s));
   }
-  int32_t st = 0;
-  HIPC(hipMemcpyAsync(out, d_sum, 48, hipMemcpyDeviceToHost, s));
-  HIPC(hipMemcpyAsync(&st, d_st + 1, 4, hipMemcpyDeviceToHost, s));
-  HIPC(hipStreamSynchronize(s));
-  return local ? local : st;
-}
-
-// Device-resident form of bls381_aggregate_pubkeys_sharded (include/bls381.h): this rank's keys
-// are already in HBM and every rank receives the aggregate and the status in HBM, on the caller's
-// stream; the call returns with its work queued (no host copy, no synchronisation).  Same protocol:
-// this rank's partial (compressed, 48 zero bytes on an error), all-gathered, decoded and summed on
-// rank 0 with the strict codec, broadcast.
-static constexpr size_t SHARDED_MAX_RANKS = 4096;
-
-size_t bls381_aggregate_pubkeys_sharded_device_workspace_size(size_t n_local) {
-  return bls381_aggregate_pubkeys_batch_workspace_size(1, n_local) +
-         bls381_aggregate_pubkeys_batch_workspace_size(1, SHARDED_MAX_RANKS);
+  HIPC(hipMemcpyAsync(d_out48, d_sum, 48, hipMemcpyDeviceToDevice, s));
+  HIPC(hipMemcpyAsync(d_status, d_st, 4, hipMemcpyDeviceToDevice, s));
+  if (cm->rows_ev) HIPC(hipEventRecord(cm->rows_ev, s));
+  return local;
 }
 
 int bls381_aggregate_pubkeys_sharded_device(size_t n_local, const uint8_t* d_pks, uint8_t* d_out48,
@@ -2724,62 +2767,51 @@ int bls381_aggregate_pubkeys_sharded_device(size_t n_local, const uint8_t* d_pks
   if (!cm) return rc;
   RcclApi* api = cm->virt ? nullptr : rccl_api();
   if (!cm->virt && !api) return BLS381_ENODEV;
+  return agg_sharded_impl(c, cm, api, n_local, d_pks, d_out48, d_status, d_workspace, (hipStream_t)stream);
+}
+
+int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[48]) {
+  // the device form's protocol over this rank's contiguous range (sizes differing by at most one,
+  // sharding.shard_range; a virtual communicator takes the whole call), copied in from host memory
+  if (!out || (n && !pks)) return BLS381_EARG;
+  int rc = 0;
+  Ctx* c = get_ctx(&rc);
+  if (!c) return rc;
+  std::lock_guard<std::mutex> clk(g_comm_mu);
+  Comm* cm = comm_ctx(&rc);
+  if (!cm) return rc;
+  RcclApi* api = cm->virt ? nullptr : rccl_api();
+  if (!cm->virt && !api) return BLS381_ENODEV;
+  if (cm->rows_ev) (void)hipEventSynchronize(cm->rows_ev);   // a device-form call may still use the rows
   const size_t R = (size_t)cm->nranks;
-  if (R > SHARDED_MAX_RANKS) { t_err = "too many ranks for the device form"; return BLS381_EARG; }
-  hipStream_t s = (hipStream_t)stream;
-  uint8_t* d_rows;   // R partials, then this rank's own, then the sum (48 B) and statuses
-  if ((rc = comm_rows(cm, 48 * R + 48 + 64 + 64, &d_rows))) return rc;
-  uint8_t* d_sum = d_rows + 48 * R + 48;
-  int32_t* d_st = (int32_t*)(d_sum + 64);
-  if (cm->rows_ev) (void)hipStreamWaitEvent(s, cm->rows_ev, 0);   // before any collective: no early return
-  const size_t ws_local = bls381_aggregate_pubkeys_batch_workspace_size(1, n_local);
-  uint8_t* ws_root = (uint8_t*)d_workspace + ws_local;
-  const size_t ws_root_cap = bls381_aggregate_pubkeys_batch_workspace_size(1, SHARDED_MAX_RANKS);
-  // virtual: one process plays every rank over the whole call, split as the host form splits it
-  const size_t base = n_local / R, extra = n_local % R;
-  int local = 0;
-  for (int r = first_rank(cm); r <= last_rank(cm); ++r) {
-    const size_t rr = (size_t)r;
-    uint8_t* part = cm->virt ? d_rows + 48 * rr : d_rows + 48 * R;
-    const size_t lo = cm->virt ? rr * base + (rr < extra ? rr : extra) : 0;
-    const size_t cnt = cm->virt ? base + (rr < extra ? 1 : 0) : n_local;
-    const int lrc = local_stage([&]() -> int {
-      const uint32_t off1[2] = {0, (uint32_t)cnt};
-      int e;
-      // the ranks of a virtual communicator reuse the workspace in stream order
-      if ((e = agg_batch_impl(c, 0, 1, off1, cnt, d_pks + 48 * lo, part, d_st, d_workspace, ws_local, s,
-                              policy_flags(0))))
-        return e;
-      LAUNCH("zero_if_error", s, dim3(1), dim3(64), k_zero_if_error, (const int32_t*)d_st, part, 48u);
-      return 0;
-    });
-    if (lrc) {
-      (void)hipMemsetAsync(part, 0, 48, s);   // 48 zero bytes: not an encoding, the sum is flagged
-      if (!local) local = lrc;
-    }
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipStream_t s = c->stream;
+  const size_t base = n / R, extra = n % R, rr = (size_t)cm->rank;
+  const size_t lo = cm->virt ? 0 : rr * base + (rr < extra ? rr : extra);
+  const size_t cnt = cm->virt ? n : base + (rr < extra ? 1 : 0);
+  const size_t wsl = bls381_aggregate_pubkeys_sharded_device_workspace_size(cnt);
+  // result and status in the rows buffer's unused tail (the protocol uses its head)
+  uint8_t* d_res = cm->rows + cm->rows_cap - 64;
+  int local = ensure_ws(c, align256(48 * cnt + 1) + wsl);
+  const uint8_t* d_in = nullptr;
+  void* w = nullptr;
+  if (!local) {
+    Bump b(c->ws, c->ws_cap);
+    uint8_t* d_pks = b.take<uint8_t>(48 * cnt + 1);
+    w = b.take<uint8_t>(wsl);
+    if (cnt && hipMemcpyAsync(d_pks, pks + 48 * lo, 48 * cnt, hipMemcpyHostToDevice, s) != hipSuccess)
+      local = fail("hipMemcpyAsync", hipGetLastError());
+    d_in = d_pks;
   }
-  if (local && cm->virt) return local;
-  if (!cm->virt) NCCLC(api, api->all_gather(d_rows + 48 * R, d_rows, 48, ncclUint8, cm->comm, s));
-  if (is_root(cm)) {
-    const int root = local_stage([&]() -> int {
-      const uint32_t offR[2] = {0, (uint32_t)R};
-      return agg_batch_impl(c, 0, 1, offR, R, d_rows, d_sum, d_st + 1, ws_root, ws_root_cap, s, 0);
-    });
-    if (root) {
-      static const int32_t err = BLS381_EHIP;   // a copy source that outlives the queued copy
-      (void)hipMemsetAsync(d_sum, 0, 48, s);
-      (void)hipMemcpyAsync(d_st + 1, &err, 4, hipMemcpyHostToDevice, s);
-      if (!local) local = root;
-    }
-  }
-  if (!cm->virt) {
-    NCCLC(api, api->broadcast(d_sum, d_sum, 48, ncclUint8, 0, cm->comm, s));
-    NCCLC(api, api->broadcast(d_st + 1, d_st + 1, 4, ncclUint8, 0, cm->comm, s));
-  }
-  HIPC(hipMemcpyAsync(d_out48, d_sum, 48, hipMemcpyDeviceToDevice, s));
-  HIPC(hipMemcpyAsync(d_status, d_st + 1, 4, hipMemcpyDeviceToDevice, s));
-  if (cm->rows_ev) HIPC(hipEventRecord(cm->rows_ev, s));
-  return local;
+  // a rank that cannot stage its keys still issues every collective of the call, with a flagged row
+  rc = agg_sharded_impl(c, cm, api, local ? 0 : cnt, local ? nullptr : d_in, d_res, (int32_t*)(d_res + 48),
+                        local ? (void*)(d_res - 16384) : w, s, local);
+  int32_t st = 0;
+  HIPC(hipMemcpyAsync(out, d_res, 48, hipMemcpyDeviceToHost, s));
+  HIPC(hipMemcpyAsync(&st, d_res + 48, 4, hipMemcpyDeviceToHost, s));
+  HIPC(hipStreamSynchronize(s));
+  if (local) return local;
+  return rc ? rc : st;
 }
 
 int bls381_verify_multiple_batch_sharded(size_t n_calls, const uint32_t* call_off, const uint8_t* pks,
