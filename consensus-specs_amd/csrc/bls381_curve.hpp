@@ -135,9 +135,9 @@ BLS_DEV_INLINE bool jac_to_aff(aff_t<F>& out, const jac_t<F>& p) {
 
 // Scalar multiplications are one (non-inlined) function each, with the point
 // formulas inlined into the loop, so the running point stays in registers.
-// [k] a for a 64-bit scalar, affine base, left-to-right
+// [k] a for a 64-bit scalar, affine base, left-to-right (the body, for callers that inline it)
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F> a, uint64_t k) {
+BLS_DEV_INLINE jac_t<F> jac_mul_u64_body(const aff_t<F>& a, uint64_t k) {
   jac_t<F> r = jac_from_aff(a);
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -147,6 +147,8 @@ BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F> a, uint64_t k) {
   }
   return r;
 }
+template <class F>
+BLS_NOINLINE jac_t<F> jac_mul_u64(const aff_t<F> a, uint64_t k) { return jac_mul_u64_body(a, k); }
 
 // [k0] a + [k1] s for 32-bit k0, k1 (Shamir's trick: one doubling chain, mixed additions);
 // with s = endo(a) for an endomorphism acting as [mu] this is [k0 + mu k1] a at half the
@@ -167,7 +169,7 @@ BLS_NOINLINE jac_t<F> jac_mul_2x32(const aff_t<F> a, const aff_t<F> s, uint32_t 
 
 // [k] p for a 64-bit scalar, Jacobian base
 template <class F>
-BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F> p, uint64_t k) {
+BLS_DEV_INLINE jac_t<F> jac_mul_u64_jac_body(const jac_t<F>& p, uint64_t k) {
   jac_t<F> r = p;
   int top = 63;
   while (top > 0 && !((k >> top) & 1)) --top;
@@ -177,6 +179,8 @@ BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F> p, uint64_t k) {
   }
   return r;
 }
+template <class F>
+BLS_NOINLINE jac_t<F> jac_mul_u64_jac(const jac_t<F> p, uint64_t k) { return jac_mul_u64_jac_body(p, k); }
 
 // a scalar of up to 512 bits, little-endian 32-bit words, passed by value (no pointer into the
 // caller's private memory crosses a call: DESIGN.md §10.8)

@@ -188,13 +188,24 @@ BLS_NOINLINE jac_t<E> g2_mul_e0(const jac_t<E> S) {
 // one raised to c, which is coprime to r, so "== 1" is unchanged (the reduced
 // pairing is bilinear in its G2 argument for any G1-side point; tested against
 // every torsion fixture).  Skips the [e0]S - T step of g2_mul_cofactor.
+// BLS_BP_INLINE_LADDERS=1 (measurement knob): the two [|x|] ladders inlined into g2_mul_bp instead
+// of calls.  r05: k_hash_bp's private segment 1,376 -> 1,808 B (the ladders' spills share one frame
+// with the rest of the map), so the calls stay
+#ifndef BLS_BP_INLINE_LADDERS
+#define BLS_BP_INLINE_LADDERS 0
+#endif
 template <class E>
 BLS_NOINLINE jac_t<E> g2_mul_bp(const aff_t<E> p) {
   aff_t<E> np;
   np.x = p.x;
   np.y = fp2_neg(p.y);
+#if BLS_BP_INLINE_LADDERS
+  const jac_t<E> t1 = jac_mul_u64_body(p, BLS_X_ABS);             // [|x|]P = -[x]P
+  jac_t<E> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac_body(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
+#else
   const jac_t<E> t1 = jac_mul_u64(p, BLS_X_ABS);                  // [|x|]P = -[x]P
   jac_t<E> Q0 = jac_add_aff(jac_add(jac_mul_u64_jac(t1, BLS_X_ABS), t1), np);   // [x^2 - x - 1]P
+#endif
   Q0 = jac_add(Q0, g2_psi_jac(jac_add_aff(jac_neg(t1), np)));          // + psi([x - 1]P)
   return jac_add(Q0, g2_psi_jac(g2_psi_jac(jac_dbl(jac_from_aff(p)))));  // + psi^2(2P)
 }
