@@ -15,13 +15,13 @@
 
 constexpr int ITERS = 4096;
 
-__global__ __launch_bounds__(256) void k_mad_clock(uint64_t* out, unsigned long long* stamps, uint32_t seed) {
+__global__ __launch_bounds__(256) void k_mad_clock(uint64_t* out, unsigned long long* stamps, uint32_t seed, int iters) {
   uint32_t a = seed + threadIdx.x, b = seed * 3u + blockIdx.x;
   uint64_t acc[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) acc[k] = (uint64_t)(a + k) << 7;
   const unsigned long long c0 = __builtin_readcyclecounter(), r0 = __builtin_amdgcn_s_memrealtime();
-  for (int i = 0; i < ITERS; ++i) {
+  for (int i = 0; i < iters; ++i) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       uint64_t cy;
@@ -41,17 +41,18 @@ __global__ __launch_bounds__(256) void k_mad_clock(uint64_t* out, unsigned long 
 }
 
 int main(int argc, char** argv) {
-  // clock_probe [blocks] [threads per block] [idle ms before each timed launch] [launches]
+  // clock_probe [blocks] [threads per block] [idle ms before each timed launch] [launches] [iterations]
   const int blocks = argc > 1 ? atoi(argv[1]) : 16384;
   const int threads = argc > 2 ? atoi(argv[2]) : 256;
   const int idle_ms = argc > 3 ? atoi(argv[3]) : 0;
   const int reps = argc > 4 ? atoi(argv[4]) : 1;
+  const int iters = argc > 5 ? atoi(argv[5]) : ITERS;
   const int wpb = (threads + 63) / 64;
   uint64_t* out;
   unsigned long long* st;
   CHECK(hipMalloc(&out, (size_t)blocks * 256 * 8));
   CHECK(hipMalloc(&st, (size_t)blocks * 4 * 2 * 8));
-  hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 7u);
+  hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 7u, iters);
   CHECK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
@@ -59,7 +60,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < reps; ++r) {
     if (idle_ms) usleep(1000 * idle_ms);
     CHECK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 9u);
+    hipLaunchKernelGGL(k_mad_clock, dim3(blocks), dim3(threads), 0, 0, out, st, 9u, iters);
     CHECK(hipEventRecord(e1, 0));
     CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -69,10 +70,10 @@ int main(int argc, char** argv) {
     double cyc = 0, rt = 0;
     for (int b = 0; b < blocks; ++b)
       for (int w = 0; w < wpb; ++w) { cyc += (double)h[((size_t)b * 4 + w) * 2]; rt += (double)h[((size_t)b * 4 + w) * 2 + 1]; }
-    const double macs = (double)blocks * threads * ITERS * 8;
+    const double macs = (double)blocks * threads * iters * 8;
     printf("{\"blocks\": %d, \"threads\": %d, \"idle_ms\": %d, \"ms\": %.4f, \"mad_Tops\": %.3f, \"s_memtime_ghz\": %.3f, "
            "\"cycles_per_mad_per_wave\": %.3f}\n", blocks, threads, idle_ms, ms, macs / (ms * 1e-3) / 1e12, cyc / (rt * 10.0),
-           (cyc / ((double)blocks * wpb)) / (ITERS * 8.0));
+           (cyc / ((double)blocks * wpb)) / (iters * 8.0));
   }
   return 0;
 }
