@@ -964,9 +964,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
                                                            const uint8_t* __restrict__ sig_st,
                                                            const uint32_t* __restrict__ slot, size_t nslots,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t t = item_index<4>();
-  if (t >= nt) return;
-  const bool lead = (threadIdx.x & 3u) == 0;
+  size_t t;
+  bool live;
+  if (!lat_unit<4>(nt, t, live)) return;
+  const bool lead = (threadIdx.x & 3u) == 0 && live;
   const int p = pr_odd() ? 1 : 0;
   const int32_t src = tasks[t];
   const size_t o = slot ? slot[t] : t;   // output slot (stride nslots)
@@ -993,6 +994,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
   } else {
     f = fq12_one();
   }
+  if (!live) return;
   const size_t lp = 2 * o + p;
   const int c0 = qd_hi() ? 3 : 0;
   soa_st(f_out, 2 * nslots, lp, c0 + 0, f.h.c0.v);

@@ -118,6 +118,21 @@ template <> struct soa_jac<fp2p_t> {
   }
 };
 
+// The latency kernels' lane assignment: units (items or pair tasks) of LPI lanes each.  A wave that
+// holds at least one unit keeps all 64 lanes active -- lanes past the last unit recompute it with
+// their stores masked (`live` false) -- and a wave with no unit exits.  Partially filled waves of these
+// spill-heavy kernels ran erratically slower (r05, DESIGN.md section 0: the quad FE took 2.86-3.87 ms
+// with 8 of 64 lanes in use and 2.87-2.91 ms with all 64; 1-item calls 9.3-9.5 against 8.4 ms).
+template <int LPI>
+__device__ __forceinline__ bool lat_unit(size_t n_units, size_t& u, bool& live) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (((g & ~(size_t)63) / LPI) >= n_units) return false;   // the wave's first unit
+  const size_t raw = g / LPI;
+  live = raw < n_units;
+  u = live ? raw : n_units - 1;
+  return true;
+}
+
 __device__ __forceinline__ void ld_bytes(uint8_t* dst, const uint8_t* __restrict__ src, int len) {
   for (int k = 0; k < len; ++k) dst[k] = src[k];
 }
@@ -195,15 +210,16 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_q(size_t n
                                                      uint32_t* __restrict__ out, uint8_t* __restrict__ st,
                                                      const uint32_t* __restrict__ koff, int prio) {
   if (prio) __builtin_amdgcn_s_setprio(2);
-  const size_t i = item_index<4>();
-  if (i >= n) return;
+  size_t i;
+  bool live;
+  if (!lat_unit<4>(n, i, live)) return;
   uint8_t dom[8];
   ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
   aff_t<fp2p_t> c;
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, koff ? (int)koff[i] : -1);
   aff_t<fp2p_t> h;
   const bool fin = jac_to_aff(h, g2_mul_bp_q(c));
-  if (qd_hi()) return;
+  if (qd_hi() || !live) return;
   if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
   if (fin) soa_st_g2(out, n, i, h);
 }
@@ -854,10 +870,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_q
                                                            const uint8_t* __restrict__ pk_st,
                                                            const uint32_t* __restrict__ h_aff,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t i = item_index<4>();
-  if (i >= n) return;
+  size_t i;
+  bool live;
+  if (!lat_unit<4>(n, i, live)) return;
   const bool hi = qd_hi();
-  const bool lead = (threadIdx.x & 3u) == 0;
+  const bool lead = (threadIdx.x & 3u) == 0 && live;
   const size_t lp = 2 * i + (pr_odd() ? 1 : 0);   // this lane's coefficient slot of item i
   const uint8_t ss = sig_st[i], ps = pk_st[i];
   if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[i] = ST_BAD; return; }
@@ -883,6 +900,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_q
   } else {
     f = fq12_one();
   }
+  if (!live) return;
   const int c0 = hi ? 3 : 0;
   soa_st(f_out, 2 * n, lp, c0 + 0, f.h.c0.v);
   soa_st(f_out, 2 * n, lp, c0 + 1, f.h.c1.v);
@@ -901,11 +919,12 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_o
                                                            const uint8_t* __restrict__ pk_st,
                                                            const uint32_t* __restrict__ h_aff,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  const size_t t = item_index<4>();
-  if (t >= 2 * n) return;
+  size_t t;
+  bool live;
+  if (!lat_unit<4>(2 * n, t, live)) return;
   const size_t i = t >> 1;
   const bool hpair = (t & 1) != 0;
-  const bool lead = (threadIdx.x & 3u) == 0;
+  const bool lead = (threadIdx.x & 3u) == 0 && live;
   const int p = pr_odd() ? 1 : 0;
   const uint8_t ss = sig_st[i], ps = pk_st[i];
   if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[t] = ST_BAD; return; }
@@ -926,6 +945,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_o
   } else {
     f = fq12_one();
   }
+  if (!live) return;
   const size_t lp = 2 * t + p;
   const int c0 = qd_hi() ? 3 : 0;
   soa_st(f_out, 4 * n, lp, c0 + 0, f.h.c0.v);
@@ -1030,9 +1050,10 @@ template <int NF>
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_q(size_t n, const uint32_t* __restrict__ f_in,
                                                                const uint8_t* __restrict__ st,
                                                                uint8_t* __restrict__ verdict) {
-  const size_t i = item_index<4>();
-  if (i >= n) return;
-  const bool lead = (threadIdx.x & 3u) == 0;
+  size_t i;
+  bool live;
+  if (!lat_unit<4>(n, i, live)) return;
+  const bool lead = (threadIdx.x & 3u) == 0 && live;
   bool ok = true;
   for (int k = 0; k < NF; ++k) ok = ok && st[NF * i + k] == ST_OK;
   if (!ok) { if (lead) verdict[i] = 0; return; }
@@ -1058,9 +1079,10 @@ template <int NF>
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_o(size_t n, const uint32_t* __restrict__ f_in,
                                                                const uint8_t* __restrict__ st,
                                                                uint8_t* __restrict__ verdict) {
-  const size_t i = item_index<8>();
-  if (i >= n) return;
-  const bool lead = (threadIdx.x & 7u) == 0;
+  size_t i;
+  bool live;
+  if (!lat_unit<8>(n, i, live)) return;
+  const bool lead = (threadIdx.x & 7u) == 0 && live;
   bool ok = true;
   for (int k = 0; k < NF; ++k) ok = ok && st[NF * i + k] == ST_OK;
   if (!ok) { if (lead) verdict[i] = 0; return; }
