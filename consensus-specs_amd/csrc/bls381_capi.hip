@@ -479,9 +479,17 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
   const dim3 g2(grid_for(2 * n)), b(KBLOCK);
   if (n <= BLS_ML_OCT_MAX_N) {
     // lowest latency: one quad per Miller pair; the FE multiplies the two values of each item
-    LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
-           (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
-           w.f, w.f_st);
+    // BLS381_ML_OCTET (default 1): one octet per Miller pair (k_miller_verify_oo, 10 product steps
+    // per doubling iteration against 19 on a quad); 0 = one quad per pair (k_miller_verify_o)
+    static const int ml_octet = env_knob("BLS381_ML_OCTET", 1);
+    if (ml_octet)
+      LAUNCH("miller_loop_2oo", s, dim3(grid_for(16 * n)), b, k_miller_verify_oo, n, (const uint32_t*)w.sig_aff,
+             (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+             w.f, w.f_st);
+    else
+      LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
+             (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+             w.f, w.f_st);
     if (fe_oct(n))
       LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), b, k_final_exp_verdict_o<2>, n, (const uint32_t*)w.f,
              (const uint8_t*)w.f_st, verdicts);

@@ -954,6 +954,51 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_o
   if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
 }
 
+// k_miller_verify_o with one octet per Miller pair (miller_loop_o1_run, bls381_quad.hpp): pair task
+// t = 2i + k of item i on lanes 8t..8t+7; quad A stores f in the layout k_miller_verify_o writes.
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_oo(size_t n, const uint32_t* __restrict__ sig_aff,
+                                                            const uint8_t* __restrict__ sig_st,
+                                                            const uint32_t* __restrict__ pk_aff,
+                                                            const uint8_t* __restrict__ pk_st,
+                                                            const uint32_t* __restrict__ h_aff,
+                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  size_t t;
+  bool live;
+  if (!lat_unit<8>(2 * n, t, live)) return;
+  const size_t i = t >> 1;
+  const bool hpair = (t & 1) != 0;
+  const bool lead = (threadIdx.x & 7u) == 0 && live;
+  const int p = pr_odd() ? 1 : 0;
+  const uint8_t ss = sig_st[i], ps = pk_st[i];
+  if (ss == ST_BAD || ps == ST_BAD) { if (lead) st_out[t] = ST_BAD; return; }
+  fq12_t f;
+  bool degen = false;
+  if (hpair ? ps == ST_OK : ss == ST_OK) {
+    const uint32_t* qsrc = hpair ? h_aff : sig_aff;
+    aff_t<fp2p_t> Q;
+    Q.x = pr_make(soa_ld(qsrc, 2 * n, 2 * i + p, 0));
+    Q.y = pr_make(soa_ld(qsrc, 2 * n, 2 * i + p, 1));
+    aff_t<fp_t> P;
+    if (hpair) {
+      P = soa_ld_g1(pk_aff, n, i);
+    } else {
+      P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
+    }
+    const fq12_ml r = miller_loop_o1_run(Q, g1_prepare(P));
+    f = r.f;
+    degen = r.degenerate;
+  } else {
+    f = fq12_one();
+  }
+  if (!live || oc_b()) return;
+  const size_t lp = 2 * t + p;
+  const int c0 = qd_hi() ? 3 : 0;
+  soa_st(f_out, 4 * n, lp, c0 + 0, f.h.c0.v);
+  soa_st(f_out, 4 * n, lp, c0 + 1, f.h.c1.v);
+  soa_st(f_out, 4 * n, lp, c0 + 2, f.h.c2.v);
+  if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
+}
+
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {

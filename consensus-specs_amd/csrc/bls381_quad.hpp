@@ -427,6 +427,146 @@ __device__ __forceinline__ fq12_t miller_loop_q1(const aff_t<fp2p_t>& Q, const g
   return r.f;
 }
 
+// ----------------------------------------------- one Miller pair per octet --
+// The lowest-latency Miller loop: one pair on 8 lanes, two quads (A = lanes 8t..8t+3, B = 8t+4..8t+7)
+// that both hold T and f in the quad layout above.  Each step's independent products run on all
+// four lane pairs at once and are exchanged between the quads (lane ^ 4, ds_swizzle):
+//   line_dbl  11 products -> 3 steps (quad: 6),  f^2  12 -> 3 (6),  f * line  13 -> 4 (7)
+// so a doubling iteration is 10 product steps against 19 on a quad.  The five additions of the loop
+// run in the quad form on both quads.  A square paired with a product runs as a product of the value
+// with itself, and an Fp x Fp2 product as an Fp2 product with (x, 0): the same field elements (all
+// values stay < 2q), so the quads stay bit-identical and T and f need no exchange.
+__device__ __forceinline__ bool oc_b() { return (threadIdx.x & 4u) != 0; }
+__device__ __forceinline__ fp2p_t oc_swap(const fp2p_t& a) {
+  fp2p_t r;
+#pragma unroll
+  for (int k = 0; k < FP_LIMBS; ++k)   // bitmask mode: and 0x1f, or 0, xor 4
+    r.v.w[k] = (uint32_t)__builtin_amdgcn_ds_swizzle((int)a.v.w[k], 0x101F);
+  return r;
+}
+// quad A's and quad B's value of a split step, on both quads
+__device__ __forceinline__ void oc_both(const fp2p_t& mine, fp2p_t& a_v, fp2p_t& b_v) {
+  const bool b = oc_b();
+  const fp2p_t o = oc_swap(mine);
+  a_v = qd_sel(b, o, mine);
+  b_v = qd_sel(b, mine, o);
+}
+
+// fp6_mul_inl with its six Karatsuba products split A | B (the same formula, bit-identical)
+__device__ __forceinline__ fp6p_t fp6_mul_oct(const fp6p_t& s, const fp6p_t& t) {
+  const bool b = oc_b();
+  fp2p_t t0, t1, t2, t3, t4, t5;
+  oc_both(fp2_mul(qd_sel(b, fp2_add_lazy(s.c1, s.c2), s.c0), qd_sel(b, fp2_add_lazy(t.c1, t.c2), t.c0)), t0, t3);
+  oc_both(fp2_mul(qd_sel(b, fp2_add_lazy(s.c0, s.c1), s.c1), qd_sel(b, fp2_add_lazy(t.c0, t.c1), t.c1)), t1, t4);
+  oc_both(fp2_mul(qd_sel(b, fp2_add_lazy(s.c0, s.c2), s.c2), qd_sel(b, fp2_add_lazy(t.c0, t.c2), t.c2)), t2, t5);
+  fp6p_t r;
+  r.c0 = fp2_add_mul_xi(t0, fp2_sub2(t3, t1, t2));
+  r.c1 = fp2_add_mul_xi(fp2_sub2(t4, t0, t1), t2);
+  r.c2 = fp2_add(fp2_sub2(t5, t0, t2), t1);
+  return r;
+}
+
+__device__ __forceinline__ fq12_t fq12_sqr_oct(const fq12_t& f) {
+  const bool hi = qd_hi();
+  const fp6p_t y = qd_swap(f.h);
+  const fp6p_t u = qd_sel(hi, fp6_add(f.h, y), f.h);
+  const fp6p_t v = qd_sel(hi, fp6_add_mul_by_v(y, f.h), y);
+  const fp6p_t p = fp6_mul_oct(u, v);                 // lo: ab, hi: (a+b)(a+vb)
+  const fp6p_t o = qd_swap(p);
+  fq12_t r;
+  r.h = qd_sel(hi, fp6_dbl(o), fp6_sub2(o, p, fp6_mul_by_v(p)));
+  return r;
+}
+
+// fq12_mul_by_line_q1 with its seven product calls split A: p0..p3 | B: p4..p6 (p3 on both)
+__device__ __forceinline__ fq12_t fq12_mul_by_line_oct(const fq12_t& f, const fp2p_t& c0, const fp2p_t& c1,
+                                                       const fp2p_t& c2) {
+  const bool hi = qd_hi(), b = oc_b();
+  const fp6p_t& h = f.h;
+  fp6p_t s = fp6_add(h, qd_swap(h));
+  const fp2p_t d1 = fp2_add(c1, c2);
+  fp2p_t p0, p1, p2, p3, p4, p5, p6;
+  oc_both(fp2_mul(qd_sel(b, qd_sel(hi, s.c1, h.c2), qd_sel(hi, h.c2, h.c0)),
+                  qd_sel(b, qd_sel(hi, d1, c0), qd_sel(hi, c2, c0))), p0, p4);            // a0c0 | b2c2 ; a2c0 | s1d1
+  oc_both(fp2_mul(qd_sel(b, qd_sel(hi, fp2_add_lazy(s.c0, s.c1), s.c2), qd_sel(hi, h.c0, h.c1)),
+                  qd_sel(b, qd_sel(hi, fp2_add_lazy(c0, d1), d1), qd_sel(hi, c2, c1))), p1, p5);   // a1c1 | b0c2 ; ...
+  oc_both(fp2_mul(qd_sel(b, s.c2, qd_sel(hi, h.c1, h.c2)), qd_sel(b, c0, qd_sel(hi, c2, c1))), p2, p6);
+  p3 = fp2_mul(qd_sel(hi, s.c0, fp2_add_lazy(h.c0, h.c1)), qd_sel(hi, c0, fp2_add_lazy(c0, c1)));
+  fp6p_t X;
+  X.c0 = qd_sel(hi, fp2_mul_xi(p0), fp2_add_mul_xi(p0, p2));
+  X.c1 = qd_sel(hi, p1, fp2_sub2(p3, p0, p1));
+  X.c2 = qd_sel(hi, p2, fp2_add(p1, p4));
+  const fp6p_t Y = qd_swap(X);                       // lo: bB, hi: aA
+  const fp2p_t q5 = qd_swap(p5), q6 = qd_swap(p6);
+  fq12_t r;
+  const fp6p_t lo = fp6_add_mul_by_v(X, Y);
+  fp6p_t m;
+  m.c0 = fp2_add_mul_xi(p3, q5);
+  m.c1 = fp2_sub2(p5, p3, p4);
+  m.c2 = fp2_add(p4, q6);
+  r.h = qd_sel(hi, fp6_sub2(m, Y, X), lo);
+  return r;
+}
+
+// line_dbl_q1 in three steps: A (X^2 | Y^2) with B (Z^2 | YZ); A (h^2 | b3^2) with B (XY | XY);
+// A (XY(YY - 9b'Z^2) | YY YZ) with B (XX(-3xp) | YZ(2yp))
+__device__ __forceinline__ void line_dbl_oct(g2_proj<fp2p_t>& T, const g1_line_pre& P, fp2p_t& c0, fp2p_t& c1,
+                                             fp2p_t& c2) {
+  const bool hi = qd_hi(), b = oc_b();
+  fp2p_t s1, m1;
+  {
+    const fp2p_t xa = qd_sel(hi, T.y, T.x);
+    oc_both(fp2_mul(qd_sel(b, T.z, xa), qd_sel(b, qd_sel(hi, T.y, T.z), xa)), s1, m1);
+  }
+  const fp2p_t s1o = qd_swap(s1), m1o = qd_swap(m1);
+  const fp2p_t XX = qd_sel(hi, s1o, s1), YY = qd_sel(hi, s1, s1o);
+  const fp2p_t ZZ = qd_sel(hi, m1o, m1), YZ = qd_sel(hi, m1, m1o);
+  const fp2p_t b3 = fp2_mul_small(fp2_mul_small(fp2_mul_xi(ZZ), 3), 4);   // 3 b' Z^2
+  const fp2p_t b9 = fp2_mul_small(b3, 3);
+  c0 = fp2_sub(YY, b3);
+  const fp2p_t h = fp2_half(fp2_add(YY, b9));
+  fp2p_t s2, XY;
+  {
+    const fp2p_t xs = qd_sel(hi, b3, h);   // lo h^2 | hi (3b'Z^2)^2, as line_dbl_q1
+    oc_both(fp2_mul(qd_sel(b, T.x, xs), qd_sel(b, T.y, xs)), s2, XY);
+  }
+  fp2p_t m2, e;
+  {
+    const fp2p_t pe = pr_make(fp_sel(pr_odd(), fp_zero(), fp_sel(hi, P.y2, P.n3x)));   // (y2 | n3x, 0)
+    oc_both(fp2_mul(qd_sel(b, qd_sel(hi, YZ, XX), qd_sel(hi, YY, XY)),
+                    qd_sel(b, pe, qd_sel(hi, YZ, fp2_sub(YY, b9)))), m2, e);
+  }
+  const fp2p_t eo = qd_swap(e), m2o = qd_swap(m2), s2o = qd_swap(s2);
+  c1 = qd_sel(hi, eo, e);
+  c2 = qd_sel(hi, e, eo);
+  T.x = fp2_half(qd_sel(hi, m2o, m2));
+  T.y = fp2_sub(qd_sel(hi, s2o, s2), fp2_mul_small(qd_sel(hi, s2, s2o), 3));
+  T.z = fp2_dbl(qd_sel(hi, m2, m2o));
+}
+
+// Miller loop of one pair on an octet; returns conj(f) (x < 0) in the quad form on both quads.
+__device__ __noinline__ fq12_ml miller_loop_o1_run(const aff_t<fp2p_t> Q, const g1_line_pre P) {
+  g2_proj<fp2p_t> T;
+  T.x = Q.x; T.y = Q.y; T.z = e2_one<fp2p_t>();
+  fq12_t f = fq12_one();
+  bool first = true;
+  for (int i = 62; i >= 0; --i) {
+    fp2p_t c0, c1, c2;
+    line_dbl_oct(T, P, c0, c1, c2);
+    if (!first) f = fq12_sqr_oct(f);
+    f = fq12_mul_by_line_oct(f, c0, c1, c2);
+    first = false;
+    if ((BLS_X_ABS >> i) & 1) {
+      line_add_q1(T, Q, P, c0, c1, c2);
+      f = fq12_mul_by_line_oct(f, c0, c1, c2);
+    }
+  }
+  fq12_ml r;
+  r.degenerate = fp2_is_zero(T.z);   // T is the same on all eight lanes
+  r.f = fq12_conj(f);
+  return r;
+}
+
 // ------------------------------------------- final exponentiation on quads --
 // The latency form of final_exp (bls381_pairing.hpp): the same chain, with every
 // Fp12 step split over the two halves, for batches too small to fill the GPU
