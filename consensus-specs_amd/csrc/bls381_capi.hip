@@ -963,7 +963,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_quads(si
 // quad t, miller_loop_q1 (every step's products split over the halves).  Writes one
 // Fp12 (pair SoA over nt values) and status per task: PAIR_NONE or an infinite
 // operand is f = 1; a bad operand or a degenerate loop is ST_BAD.
-__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1(size_t nt, const int32_t* __restrict__ tasks,
+// LPI = 4: one quad per pair task (miller_loop_q1); LPI = 8: one octet per task (miller_loop_o1_run,
+// quad A stores)
+template <int LPI>
+__global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks(size_t nt, const int32_t* __restrict__ tasks,
                                                            size_t G, const uint32_t* __restrict__ h_aff,
                                                            const uint8_t* __restrict__ h_st,
                                                            const uint32_t* __restrict__ agg_aff,
@@ -972,10 +975,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
                                                            const uint8_t* __restrict__ sig_st,
                                                            const uint32_t* __restrict__ slot, size_t nslots,
                                                            uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  static_assert(LPI == 4 || LPI == 8, "quad or octet tasks");
   size_t t;
   bool live;
-  if (!lat_unit<4>(nt, t, live)) return;
-  const bool lead = (threadIdx.x & 3u) == 0 && live;
+  if (!lat_unit<LPI>(nt, t, live)) return;
+  const bool lead = (threadIdx.x & (LPI - 1u)) == 0 && live;
   const int p = pr_odd() ? 1 : 0;
   const int32_t src = tasks[t];
   const size_t o = slot ? slot[t] : t;   // output slot (stride nslots)
@@ -998,11 +1002,17 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_tasks_q1
       Q.y = pr_make(soa_ld(sig_aff, 2 * ncalls, 2 * c + p, 1));
       P.x = G1_VGEN_X_M; P.y = G1_VGEN_NEGY_M;
     }
-    f = miller_loop_q1(Q, g1_prepare(P), degen);
+    if (LPI == 8) {
+      const fq12_ml r = miller_loop_o1_run(Q, g1_prepare(P));
+      f = r.f;
+      degen = r.degenerate;
+    } else {
+      f = miller_loop_q1(Q, g1_prepare(P), degen);
+    }
   } else {
     f = fq12_one();
   }
-  if (!live) return;
+  if (!live || (LPI == 8 && oc_b())) return;
   const size_t lp = 2 * o + p;
   const int c0 = qd_hi() ? 3 : 0;
   soa_st(f_out, 2 * nslots, lp, c0 + 0, f.h.c0.v);
@@ -1144,7 +1154,7 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     if (!pl.tasks) {
       // large batches: the signature pairs run here, beside hash_to_G2, so the group pairs fill
       // whole quads and the main Miller launch has no partial last round of waves
-      LAUNCH("miller_sig_tasks", c->side2, dim3(grid_for(4 * ncalls)), dim3(KBLOCK), k_miller_tasks_q1, ncalls,
+      LAUNCH("miller_sig_tasks", c->side2, dim3(grid_for(4 * ncalls)), dim3(KBLOCK), k_miller_tasks<4>, ncalls,
              (const int32_t*)d_stask, G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff,
              (const uint8_t*)agg_st, ncalls, (const uint32_t*)sig_aff, (const uint8_t*)sig_st,
              (const uint32_t*)d_sslot, nf, f, st);
@@ -1167,9 +1177,16 @@ int run_vm_batch(Ctx* c, const VmPlan& pl, size_t mlen, const uint8_t* d_pks, co
     HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
   }
   if (pl.tasks) {
-    LAUNCH("miller_tasks_q1", s, dim3(grid_for(4 * nf)), dim3(KBLOCK), k_miller_tasks_q1, nf, (const int32_t*)d_qp,
-           G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
-           (const uint32_t*)sig_aff, (const uint8_t*)sig_st, (const uint32_t*)nullptr, nf, f, st);
+    // BLS381_ML_OCTET: one octet per pair task while the tasks fit one wave per SIMD
+    static const int ml_octet = env_knob("BLS381_ML_OCTET", 1);
+    if (ml_octet && nf <= 8192)
+      LAUNCH("miller_tasks_o1", s, dim3(grid_for(8 * nf)), dim3(KBLOCK), k_miller_tasks<8>, nf, (const int32_t*)d_qp,
+             G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+             (const uint32_t*)sig_aff, (const uint8_t*)sig_st, (const uint32_t*)nullptr, nf, f, st);
+    else
+      LAUNCH("miller_tasks_q1", s, dim3(grid_for(4 * nf)), dim3(KBLOCK), k_miller_tasks<4>, nf, (const int32_t*)d_qp,
+             G, (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
+             (const uint32_t*)sig_aff, (const uint8_t*)sig_st, (const uint32_t*)nullptr, nf, f, st);
   } else {
     LAUNCH("miller_quads", s, dim3(grid_for(4 * nq)), dim3(KBLOCK), k_miller_quads, nq, (const int32_t*)d_qp, G,
            (const uint32_t*)h_aff, (const uint8_t*)h_st, (const uint32_t*)agg_aff, (const uint8_t*)agg_st, ncalls,
