@@ -1118,6 +1118,35 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   if (lead) verdict[i] = one ? 1 : 0;
 }
 
+// k_final_exp_verdict_q on an octet with the Fp12 products split four ways (final_exp_oq):
+// both quads hold f; quad A's lead lane writes the verdict
+template <int NF>
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_oq(size_t n, const uint32_t* __restrict__ f_in,
+                                                                const uint8_t* __restrict__ st,
+                                                                uint8_t* __restrict__ verdict) {
+  size_t i;
+  bool live;
+  if (!lat_unit<8>(n, i, live)) return;
+  const bool lead = (threadIdx.x & 7u) == 0 && live;
+  bool ok = true;
+  for (int k = 0; k < NF; ++k) ok = ok && st[NF * i + k] == ST_OK;
+  if (!ok) { if (lead) verdict[i] = 0; return; }
+  const int p = pr_odd() ? 1 : 0;
+  const int c0 = qd_hi() ? 3 : 0;
+  const size_t nv = NF * n;
+  auto load = [&](size_t v) {
+    fq12_t g;
+    g.h.c0 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 0));
+    g.h.c1 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 1));
+    g.h.c2 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 2));
+    return g;
+  };
+  fq12_t f = load(NF * i);
+  for (int k = 1; k < NF; ++k) f = fq12_mul_oct(f, load(NF * i + k));
+  const bool one = fq12_is_one(final_exp_oq(f));
+  if (lead) verdict[i] = one ? 1 : 0;
+}
+
 // The octet form (final_exp_o, 8 lanes per item) of k_final_exp_verdict_q: the lowest
 // latency, for single calls and small batches (BLS381_FE_OCT=1; off by default until measured).
 template <int NF>

@@ -748,6 +748,93 @@ __device__ inline fq12_t final_exp_q(const fq12_t f) {
   return fq12_mul(c, t3);
 }
 
+
+// ---- the final exponentiation on an octet, products split (k_final_exp_verdict_oq) ----
+// The compressed squarings stay in the quad form on both quads (the four-way split of
+// cyc_exp_x_o below costs more in exchanges than it saves); every Fp12 product runs its Fp6
+// products over the four lane pairs: fq12_mul 9 product steps -> 5.
+// fp6_mul_split with its three products per half split A: 0, 2 | B: 1, 2 (the same values)
+__device__ __forceinline__ fp6p_t fp6_mul_split_oct(const fp6p_t& s, const fp6p_t& t) {
+  const bool hi = qd_hi(), b = oc_b();
+  const fp2p_t x0 = qd_sel(hi, fp2_add_lazy(s.c1, s.c2), s.c0), y0 = qd_sel(hi, fp2_add_lazy(t.c1, t.c2), t.c0);
+  const fp2p_t x1 = qd_sel(hi, fp2_add_lazy(s.c0, s.c1), s.c1), y1 = qd_sel(hi, fp2_add_lazy(t.c0, t.c1), t.c1);
+  const fp2p_t x2 = qd_sel(hi, fp2_add_lazy(s.c0, s.c2), s.c2), y2 = qd_sel(hi, fp2_add_lazy(t.c0, t.c2), t.c2);
+  fp2p_t p[3];
+  oc_both(fp2_mul(qd_sel(b, x1, x0), qd_sel(b, y1, y0)), p[0], p[1]);
+  p[2] = fp2_mul(x2, y2);
+  fp2p_t o[3];
+  for (int k = 0; k < 3; ++k) o[k] = qd_swap(p[k]);
+  const fp2p_t t0 = qd_sel(hi, o[0], p[0]), t1 = qd_sel(hi, o[1], p[1]), t2 = qd_sel(hi, o[2], p[2]);
+  const fp2p_t t3 = qd_sel(hi, p[0], o[0]), t4 = qd_sel(hi, p[1], o[1]), t5 = qd_sel(hi, p[2], o[2]);
+  fp6p_t r;
+  r.c0 = fp2_add_mul_xi(t0, fp2_sub2(t3, t1, t2));
+  r.c1 = fp2_add_mul_xi(fp2_sub2(t4, t0, t1), t2);
+  r.c2 = fp2_add(fp2_sub2(t5, t0, t2), t1);
+  return r;
+}
+
+__device__ __forceinline__ fq12_t fq12_mul_oct(const fq12_t& f, const fq12_t& g) {
+  const bool hi = qd_hi();
+  const fp6p_t yf = qd_swap(f.h), yg = qd_swap(g.h);
+  const fp6p_t p = fp6_mul_oct(f.h, g.h);            // lo: ac, hi: bd
+  const fp6p_t m = fp6_mul_split_oct(fp6_add(f.h, yf), fp6_add(g.h, yg));
+  const fp6p_t o = qd_swap(p);
+  fq12_t r;
+  r.h = qd_sel(hi, fp6_sub2(m, o, p), fp6_add_mul_by_v(p, o));
+  return r;
+}
+
+__device__ __noinline__ fq12_t cyc_exp_x_gs_oq(const fq12_t f) {
+  fq12_t r = f;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS[s]; j > 0; --j) r = fq12_sqr_oct(r);
+    if (s < 5) r = fq12_mul_oct(r, f);
+  }
+  return fq12_conj(r);
+}
+
+__device__ __noinline__ fq12_t cyc_exp_x_oq(const fq12_t f) {
+  const bool hi = qd_hi();
+  cq_t snap[6];
+  cq_t g = cq_compress(f);
+  bool zero = false;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cq_sqr(g);
+    snap[s] = g;
+    zero = zero | fp2_is_zero(cq_g2(g));
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs_oq(f);
+  fp2p_t pre[6];
+  pre[0] = fp2_mul_small(cq_g2(snap[0]), 4);
+  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(cq_g2(snap[s]), 4));
+  fp2p_t inv = fp2_inv(pre[5]);
+  fq12_t r;
+  for (int s = 5; s >= 0; --s) {
+    fp2p_t is = inv;
+    if (s) {
+      const fp2p_t p = fp2_mul(inv, qd_sel(hi, fp2_mul_small(cq_g2(snap[s]), 4), pre[s - 1]));
+      const fp2p_t po = qd_swap(p);
+      is = qd_sel(hi, po, p);
+      inv = qd_sel(hi, p, po);
+    }
+    const fq12_t x = cq_decompress(snap[s], is);
+    r = (s == 5) ? x : fq12_mul_oct(r, x);
+  }
+  return fq12_conj(r);
+}
+
+__device__ inline fq12_t final_exp_oq(const fq12_t f) {
+  fq12_t t = fq12_mul_oct(fq12_conj(f), fq12_inv(f));
+  t = fq12_mul_oct(fq12_frob(t, 2), t);
+  fq12_t a = fq12_mul_oct(cyc_exp_x_oq(t), fq12_conj(t));
+  a = fq12_mul_oct(cyc_exp_x_oq(a), fq12_conj(a));
+  const fq12_t b = fq12_mul_oct(cyc_exp_x_oq(a), fq12_frob(a, 1));
+  const fq12_t bx2 = cyc_exp_x_oq(cyc_exp_x_oq(b));
+  const fq12_t c = fq12_mul_oct(fq12_mul_oct(bx2, fq12_frob(b, 2)), fq12_conj(b));
+  const fq12_t t3 = fq12_mul_oct(fq12_sqr_oct(t), t);
+  return fq12_mul_oct(c, t3);
+}
+
 // ------------------------------------- compressed squarings on a lane octet --
 // The lowest-latency form of cyc_exp_x for single calls: an item's FE runs on 8 lanes,
 // two quads holding the same fq12_t (every Fp12 step is computed on both, identically),
