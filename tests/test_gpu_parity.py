@@ -403,6 +403,30 @@ def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
     assert tiled == [base[i % len(cases)] for i in range(n)]
 
 
+@pytest.mark.parametrize("policy", ["pyecc", "strict"])
+def test_latency_batches_every_small_size(native, golden, torsion, policy):
+    """The latency kernels keep whole waves active and mask the stores of lanes past the last item
+    (lat_unit, bls381_kernels.hpp): batches of every size around the wave boundaries of their layouts
+    (16 items per wave on quads, 8 on octets, 4 per wave for the octet Miller pairs), at rotating
+    offsets into the golden + torsion verify cases, give each case's fixture verdict."""
+    _, gb = golden
+    gcol = "expected" if policy == "pyecc" else "expected_strict"
+    cases = [(c, c[gcol]) for c in gb["verify"] if len(bytes.fromhex(c["message"])) == 32]
+    cases += [(c, c["expected_" + policy]) for c in torsion["verify"]]
+    native.set_subgroup_policy(policy)
+    try:
+        for n in (1, 2, 3, 4, 5, 7, 8, 9, 15, 16, 17, 31, 33):
+            for off in (0, 5):
+                items = [cases[(off + i) % len(cases)] for i in range(n)]
+                got = list(native.verify_batch(b"".join(bytes.fromhex(c["pubkey"]) for c, _ in items),
+                                               b"".join(bytes.fromhex(c["message"]) for c, _ in items),
+                                               b"".join(bytes.fromhex(c["signature"]) for c, _ in items),
+                                               b"".join(int(c["domain"]).to_bytes(8, "big") for c, _ in items)))
+                assert got == [e for _, e in items], (n, off)
+    finally:
+        native.set_subgroup_policy("pyecc")
+
+
 @pytest.mark.parametrize("n", [4096, 12000, 20000])
 def test_batch_full_size_roundtrip(native, n):
     """Signed items (sign -> verify round trip), 1/4 tampered, at sizes that run each Miller /
