@@ -866,7 +866,14 @@ __device__ __forceinline__ cq_t co_exit(const fp2p_t& s) {
 __device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
   const bool up = od_upper(), p = pr_odd();
   const uint32_t pair = (threadIdx.x >> 1) & 3u;
-  const bool sq = pair == 0 || pair == 3, xp = pair == 1;
+  // the pair's role as opaque lane masks: on the plain comparisons the compiler rebuilt the operand
+  // selects below as a branch tree over `pair` (268 exec-mask branches per squaring; r05
+  // tools/csqr_lat.hip, one item: 15.0k -> 11.9k cycles per squaring with the masks, against 10.1k for
+  // the quad form, which therefore stays the default: BLS381_FE_OCT=2)
+  uint32_t sqm = ((pair ^ (pair >> 1)) & 1u) - 1u;            // pairs 0, 3: all ones
+  uint32_t xpm = 0u - ((((pair ^ 1u) - 1u) >> 31) & 1u);      // pair 1: all ones
+  asm volatile("" : "+v"(sqm), "+v"(xpm));
+  const bool sq = sqm != 0, xp = xpm != 0;
   const fp_t a = pr_dpp<DPP_HSWAP>(g.v);
   const fp_t b = pr_dpp<DPP_HSWAP>(od_cross(g.v));
   const fp_t X = fp_sel(up, b, a), Y = fp_sel(up, a, b);     // (g2, g3) or (g4, g5)
