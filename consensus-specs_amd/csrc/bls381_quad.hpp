@@ -868,8 +868,8 @@ __device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
   const uint32_t pair = (threadIdx.x >> 1) & 3u;
   // the pair's role as opaque lane masks: on the plain comparisons the compiler rebuilt the operand
   // selects below as a branch tree over `pair` (268 exec-mask branches per squaring; r05
-  // tools/csqr_lat.hip, one item: 15.0k -> 11.9k cycles per squaring with the masks, against 10.1k for
-  // the quad form, which therefore stays the default: BLS381_FE_OCT=2)
+  // tools/csqr_lat.hip, one item: 15.0k -> 11.9k cycles per squaring with the masks; the operand prep
+  // below as word blends instead of selects: 7.2k, against 10.1k for the quad form -> BLS381_FE_OCT=3)
   uint32_t sqm = ((pair ^ (pair >> 1)) & 1u) - 1u;            // pairs 0, 3: all ones
   uint32_t xpm = 0u - ((((pair ^ 1u) - 1u) >> 31) & 1u);      // pair 1: all ones
   asm volatile("" : "+v"(sqm), "+v"(xpm));
@@ -887,19 +887,24 @@ __device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
     lv_from(u, fp_reduce_lc<2>(us));   // Y0 -+ Y1 reduced (the square's operand)
   }
   lv_t a1, b1, a2, b2, a3, b3;
+  const uint32_t pm = 0u - (uint32_t)p;
 #pragma unroll
   for (int k = 0; k < 14; ++k) {
-    const int32_t x0 = (int32_t)X0.w[k], x1 = (int32_t)X1.w[k], y0 = (int32_t)Y0.w[k], y1 = (int32_t)Y1.w[k];
-    const int32_t ys = y0 + y1, yd = y0 - y1;
+    const uint32_t x0 = X0.w[k], x1 = X1.w[k], y0 = Y0.w[k], y1 = Y1.w[k];
+    const uint32_t ys = y0 + y1, yd = y0 - y1;
     // SQ:    Re (x0+x1)(x0-x1) + u^2 - 2 y1^2,  Im 2 x0 x1 + u^2 - 2 y1^2   (lz_sqr_xisqr)
     // XPROD: Re x0 (y0-y1) - x1 (y0+y1),        Im x0 (y0+y1) + x1 (y0-y1) (lz_xi_mul)
     // PROD:  Re x0 y0 - x1 y1,                  Im x0 y1 + x1 y0           (lz_mul)
-    a1[k] = sq ? (p ? 2 * x0 : x0 + x1) : x0;
-    b1[k] = sq ? (p ? x1 : x0 - x1) : (xp ? (p ? ys : yd) : (p ? y1 : y0));
-    a2[k] = sq ? u[k] : x1;
-    b2[k] = sq ? u[k] : (xp ? (p ? yd : -ys) : (p ? y0 : -y1));
-    a3[k] = sq ? -2 * y1 : 0;
-    b3[k] = sq ? y1 : 0;
+    // (two's-complement words blended with the lane masks: no per-lane branches)
+    auto blend = [](uint32_t m, uint32_t a, uint32_t b) { return b ^ (m & (a ^ b)); };   // m ? a : b
+    const uint32_t t_sq = blend(pm, x1, x0 - x1), t_xp = blend(pm, ys, yd), t_pr = blend(pm, y1, y0);
+    const uint32_t u_xp = blend(pm, yd, 0u - ys), u_pr = blend(pm, y0, 0u - y1);
+    a1[k] = (int32_t)(x0 + (sqm & blend(pm, x0, x1)));
+    b1[k] = (int32_t)blend(sqm, t_sq, blend(xpm, t_xp, t_pr));
+    a2[k] = (int32_t)blend(sqm, (uint32_t)u[k], x1);
+    b2[k] = (int32_t)blend(sqm, (uint32_t)u[k], blend(xpm, u_xp, u_pr));
+    a3[k] = (int32_t)(sqm & (0u - 2u * y1));
+    b3[k] = (int32_t)(sqm & y1);
   }
   // columns: 3 x 14 products < 2^57 (< 2^62.4) plus the reduction's < 2^59.8; values in
   // (-16 q^2, 12 q^2) as for lz_sqr_xisqr (the product outputs: |X| < 16 q^2)
@@ -941,6 +946,49 @@ __device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t f) {
     r = (s == 5) ? x : fq12_mul(r, x);
   }
   return fq12_conj(r);
+}
+
+// cyc_exp_x_oq with the squarings on the octet as well (co_sqr) -- the single-call FE (BLS381_FE_OCT=3)
+__device__ __noinline__ fq12_t cyc_exp_x_oo(const fq12_t f) {
+  const bool hi = qd_hi();
+  cq_t snap[6];
+  fp2p_t g = co_enter(cq_compress(f));
+  bool zero = false;
+  for (int s = 0; s < 6; ++s) {
+    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = co_sqr(g);
+    snap[s] = co_exit(g);
+    zero = zero | fp2_is_zero(cq_g2(snap[s]));
+  }
+  if (BLS_ANY(zero)) return cyc_exp_x_gs_oq(f);
+  fp2p_t pre[6];
+  pre[0] = fp2_mul_small(cq_g2(snap[0]), 4);
+  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(cq_g2(snap[s]), 4));
+  fp2p_t inv = fp2_inv(pre[5]);
+  fq12_t r;
+  for (int s = 5; s >= 0; --s) {
+    fp2p_t is = inv;
+    if (s) {
+      const fp2p_t p = fp2_mul(inv, qd_sel(hi, fp2_mul_small(cq_g2(snap[s]), 4), pre[s - 1]));
+      const fp2p_t po = qd_swap(p);
+      is = qd_sel(hi, po, p);
+      inv = qd_sel(hi, p, po);
+    }
+    const fq12_t x = cq_decompress(snap[s], is);
+    r = (s == 5) ? x : fq12_mul_oct(r, x);
+  }
+  return fq12_conj(r);
+}
+
+__device__ inline fq12_t final_exp_oo(const fq12_t f) {
+  fq12_t t = fq12_mul_oct(fq12_conj(f), fq12_inv(f));
+  t = fq12_mul_oct(fq12_frob(t, 2), t);
+  fq12_t a = fq12_mul_oct(cyc_exp_x_oo(t), fq12_conj(t));
+  a = fq12_mul_oct(cyc_exp_x_oo(a), fq12_conj(a));
+  const fq12_t b = fq12_mul_oct(cyc_exp_x_oo(a), fq12_frob(a, 1));
+  const fq12_t bx2 = cyc_exp_x_oo(cyc_exp_x_oo(b));
+  const fq12_t c = fq12_mul_oct(fq12_mul_oct(bx2, fq12_frob(b, 2)), fq12_conj(b));
+  const fq12_t t3 = fq12_mul_oct(fq12_sqr_oct(t), t);
+  return fq12_mul_oct(c, t3);
 }
 
 // final_exp_q with cyc_exp_x_o: both quads of the octet hold f
