@@ -228,9 +228,10 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
 #endif
 int env_knob(const char* name, int def);
 // BLS381_FE_OCT: 0 = quads (k_final_exp_verdict_q), 1 = octets with the squarings split four ways
-// (k_final_exp_verdict_o), 2 (default) = octets with the Fp12 products split (k_final_exp_verdict_oq)
+// (k_final_exp_verdict_o), 2 = octets with the Fp12 products split (k_final_exp_verdict_oq<.., 0>),
+// 3 (default) = both (k_final_exp_verdict_oq<.., 1>)
 int fe_oct_mode() {
-  static const int m = env_knob("BLS381_FE_OCT", 2);
+  static const int m = env_knob("BLS381_FE_OCT", 3);
   return m;
 }
 bool fe_oct(size_t n) { return fe_oct_mode() && n <= BLS_FE_OCT_MAX_N; }
@@ -260,7 +261,9 @@ int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* 
            verdicts);
     return 0;
   }
-  if (fe_oct(n) && fe_oct_mode() == 2)
+  if (fe_oct(n) && fe_oct_mode() == 3)
+    LAUNCH("final_exp_oo", s, dim3(grid_for(8 * n)), dim3(KBLOCK), (k_final_exp_verdict_oq<1, 1>), n, f, st, verdicts);
+  else if (fe_oct(n) && fe_oct_mode() == 2)
     LAUNCH("final_exp_oq", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_oq<1>, n, f, st, verdicts);
   else if (fe_oct(n))
     LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_o<1>, n, f, st, verdicts);
@@ -495,7 +498,10 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
       LAUNCH("miller_loop_2o", s, dim3(grid_for(8 * n)), b, k_miller_verify_o, n, (const uint32_t*)w.sig_aff,
              (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
              w.f, w.f_st);
-    if (fe_oct(n) && fe_oct_mode() == 2)
+    if (fe_oct(n) && fe_oct_mode() == 3)
+      LAUNCH("final_exp_oo", s, dim3(grid_for(8 * n)), b, (k_final_exp_verdict_oq<2, 1>), n, (const uint32_t*)w.f,
+             (const uint8_t*)w.f_st, verdicts);
+    else if (fe_oct(n) && fe_oct_mode() == 2)
       LAUNCH("final_exp_oq", s, dim3(grid_for(8 * n)), b, k_final_exp_verdict_oq<2>, n, (const uint32_t*)w.f,
              (const uint8_t*)w.f_st, verdicts);
     else if (fe_oct(n))

@@ -1120,7 +1120,8 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
 
 // k_final_exp_verdict_q on an octet with the Fp12 products split four ways (final_exp_oq):
 // both quads hold f; quad A's lead lane writes the verdict
-template <int NF>
+// SQ = 1: the compressed squarings on the octet too (final_exp_oo, BLS381_FE_OCT=3)
+template <int NF, int SQ = 0>
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_oq(size_t n, const uint32_t* __restrict__ f_in,
                                                                 const uint8_t* __restrict__ st,
                                                                 uint8_t* __restrict__ verdict) {
@@ -1143,7 +1144,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   };
   fq12_t f = load(NF * i);
   for (int k = 1; k < NF; ++k) f = fq12_mul_oct(f, load(NF * i + k));
-  const bool one = fq12_is_one(final_exp_oq(f));
+  const bool one = fq12_is_one(SQ ? final_exp_oo(f) : final_exp_oq(f));
   if (lead) verdict[i] = one ? 1 : 0;
 }
 

@@ -1321,13 +1321,15 @@ print("octet fe ok")
 """
 
 
-def test_octet_final_exponentiation_knob():
-    """BLS381_FE_OCT=1 (read once per process, so in a child process): the octet-layout
-    final exponentiation (k_final_exp_verdict_o, squarings split over four lane pairs) gives
-    the fixture verdicts for bls_verify batches (one and two values per item) and
-    verify_multiple batches."""
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_octet_final_exponentiation_knob(mode):
+    """BLS381_FE_OCT=1 / 2 (read once per process, so in a child process): the non-default
+    octet-layout final exponentiations (k_final_exp_verdict_o, squarings split over four lane
+    pairs; k_final_exp_verdict_oq<.., 0>, products split, squarings on quads) give the fixture
+    verdicts for bls_verify batches (one and two values per item) and verify_multiple batches.
+    The default (3) runs in every other test."""
     import subprocess
-    env = dict(os.environ, BLS381_FE_OCT="1")
+    env = dict(os.environ, BLS381_FE_OCT=mode)
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", _OCT_SCRIPT, root], env=env, capture_output=True, text=True,
                        timeout=110)
