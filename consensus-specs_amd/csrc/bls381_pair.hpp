@@ -347,6 +347,38 @@ __device__ inline fp2p_t fp2_inv(const fp2p_t a) {
   return pr_make(fp_sel(pr_odd(), fp_neg(r), r));
 }
 
+// a^((q-3)/4) = a^(q >> 2) for an a held on both lanes of the pair, right to left: the even lane
+// squares a^(2^i), the odd lane multiplies the set bits' powers (broadcast by DPP) into the
+// product, so each of the 379 exponent bits costs one product time, against 375 squarings + 86
+// products when both lanes run fp_pow_qm3d4's window chain (BLS_POW_PAIR=0).  The exponent is a
+// constant: the bit tests are wave-uniform (scalar branches).  Result on both lanes.
+#ifndef BLS_POW_PAIR
+#define BLS_POW_PAIR 1
+#endif
+__device__ __noinline__ fp_t fp_pow_qm3d4_pair(const fp_t a) {
+#if BLS_POW_PAIR
+  const bool odd = pr_odd();
+  fp_t r = odd ? FP_ONE_M : a;   // even lane: a^(2^i); odd lane: the running product
+#pragma unroll 1
+  for (int i = 0; i < 379; ++i) {
+    const int b = i + 2;
+    const fp_t pw = pr_dpp<DPP_EVEN>(r);
+    if ((Q_LIMBS[b / 28] >> (b % 28)) & 1u)
+      r = fp_mul(odd ? r : pw, pw);
+    else
+      r = fp_sel(odd, r, fp_sqr(r));
+  }
+  return pr_dpp<DPP_ODD>(r);
+#else
+  return fp_pow_qm3d4(a);
+#endif
+}
+
+__device__ __forceinline__ bool fp_sqrt_pair(fp_t& r, const fp_t& a) {
+  r = fp_mul(fp_pow_qm3d4_pair(a), a);
+  return fp_eq(fp_sqr(r), a);
+}
+
 // Complex-method square root (same steps as the one-lane fp2_sqrt, so the
 // spec's selection rule picks the same root).  With gamma = sqrt(a0^2 + a1^2)
 // and delta = (a0 + gamma)/2 (both lanes), t = delta^((q+1)/4) and 1/t come
@@ -369,9 +401,9 @@ __device__ __forceinline__ bool fp2_sqrt(fp2p_t& r, const fp2p_t& a) {
   const fp_t t2 = fp_sqr(a.v);
   const fp_t alpha = fp_add(t2, pr_dpp<DPP_SWAP>(t2));
   fp_t gamma;
-  if (!fp_sqrt(gamma, alpha)) return false;
+  if (!fp_sqrt_pair(gamma, alpha)) return false;
   const fp_t delta = fp_half(fp_add(a0, gamma));
-  const fp_t u = fp_pow_qm3d4(delta);
+  const fp_t u = fp_pow_qm3d4_pair(delta);
   const fp_t t = fp_mul(u, delta);                                   // delta^((q+1)/4)
   const fp_t other = fp_mul(a1, fp_half(fp_mul(fp_sqr(u), t)));     // a1 / (2t)
   const bool sq = fp_eq(fp_sqr(t), delta);
