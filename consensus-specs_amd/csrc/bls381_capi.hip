@@ -386,7 +386,11 @@ int launch_hash_g2(hipStream_t s, size_t n, const uint8_t* msgs, uint32_t mlen, 
 int launch_hash_koff(hipStream_t s, size_t n, const uint8_t* msgs, uint32_t mlen, const uint8_t* doms, int dom_stride,
                      uint32_t* h_aff, uint8_t* st, const uint32_t* koff, int prio) {
   static const size_t quad_max = (size_t)env_knob("BLS381_HASH_QUAD_MAX_N", 8192);
-  if (n <= quad_max)
+  static const int oct = env_knob("BLS381_HASH_OCT", 1);   // the doublings on octets (k_hash_g2_o)
+  if (n <= quad_max && oct)
+    LAUNCH("hash_to_g2_o", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_hash_g2_o, n, msgs, mlen, doms, dom_stride, h_aff,
+           st, koff, prio);
+  else if (n <= quad_max)
     LAUNCH("hash_to_g2_q", s, dim3(grid_for(4 * n)), dim3(KBLOCK), k_hash_g2_q, n, msgs, mlen, doms, dom_stride, h_aff,
            st, koff, prio);
   else

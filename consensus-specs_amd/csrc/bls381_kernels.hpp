@@ -224,6 +224,26 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_q(size_t n
   if (fin) soa_st_g2(out, n, i, h);
 }
 
+// k_hash_g2_q with the cofactor map's doublings on lane octets (g2_mul_bp_o); quad A's lo pair stores
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_o(size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                     const uint8_t* __restrict__ doms, int dom_stride,
+                                                     uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                     const uint32_t* __restrict__ koff, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
+  size_t i;
+  bool live;
+  if (!lat_unit<8>(n, i, live)) return;
+  uint8_t dom[8];
+  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
+  aff_t<fp2p_t> c;
+  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom, koff ? (int)koff[i] : -1);
+  aff_t<fp2p_t> h;
+  const bool fin = jac_to_aff(h, g2_mul_bp_o(c));
+  if (oc_b() || qd_hi() || !live) return;
+  if (st && !pr_odd()) st[i] = fin ? ST_OK : ST_INF;
+  if (fin) soa_st_g2(out, n, i, h);
+}
+
 // One-lane forms of decode_g2 and hash_to_g2 (fp2_t arithmetic on one lane per item:
 // Karatsuba Fp2 products, and the Fp-only square roots computed once per item instead of
 // on both lanes of a pair).  They write the lane-pair SoA layout the pair kernels read.

@@ -452,6 +452,74 @@ __device__ __forceinline__ void oc_both(const fp2p_t& mine, fp2p_t& a_v, fp2p_t&
   b_v = qd_sel(b, mine, o);
 }
 
+// ----------------------------------------- G2 doubling on an octet (k_hash_g2_o) --
+// The point on both quads; the doubling's independent products on the octet's four lane pairs
+// (slot = 2 * quad B + hi): X^2 | Y^2 | Y Z, then B^2 | (X + B)^2 | E^2, then E (D - X3) -- 3 product
+// times against jac_dbl_q's 4.  The additions stay in the quad form (both quads compute them).
+// The value of each of the first `nv` slots, on every lane of the octet
+template <int NV>
+__device__ __forceinline__ void oc_slots(const fp2p_t& mine, fp2p_t (&v)[NV]) {
+  const bool b = oc_b(), hi = qd_hi();
+  const fp2p_t oq = qd_swap(mine), oo = oc_swap(mine), oqo = oc_swap(oq);
+#pragma unroll
+  for (int t = 0; t < NV; ++t) {
+    const bool bb = b != (bool)(t >> 1), hh = hi != (bool)(t & 1);
+    v[t] = qd_sel(bb, qd_sel(hh, oqo, oo), qd_sel(hh, oq, mine));
+  }
+}
+__device__ __forceinline__ fp2p_t oc_pick(const fp2p_t& a0, const fp2p_t& a1, const fp2p_t& a2, const fp2p_t& a3) {
+  const bool b = oc_b(), hi = qd_hi();
+  return qd_sel(b, qd_sel(hi, a3, a2), qd_sel(hi, a1, a0));
+}
+
+__device__ __forceinline__ jac_t<fp2p_t> jac_dbl_o(const jac_t<fp2p_t>& p) {
+  fp2p_t v[3];
+  oc_slots<3>(fp2_mul(oc_pick(p.x, p.y, p.y, p.x), oc_pick(p.x, p.y, p.z, p.x)), v);   // X^2 | Y^2 | Y Z
+  const fp2p_t A = v[0], B = v[1], YZ = v[2];
+  const fp2p_t E = fp2_mul_small(A, 3);
+  const fp2p_t XpB = fp2_add(p.x, B);
+  oc_slots<3>(fp2_mul(oc_pick(B, XpB, E, B), oc_pick(B, XpB, E, B)), v);             // B^2 | (X + B)^2 | E^2
+  const fp2p_t C = v[0], XB2 = v[1], Fv = v[2];
+  const fp2p_t D = fp2_dbl(fp2_sub2(XB2, A, C));
+  jac_t<fp2p_t> r;
+  r.x = fp2_sub2(Fv, D, D);
+  r.y = fp2_sub(fp2_mul(E, fp2_sub(D, r.x)), fp2_mul_small(C, 8));
+  r.z = fp2_dbl(YZ);
+  return r;   // Z = 0 stays 0
+}
+
+__device__ __noinline__ jac_t<fp2p_t> jac_mul_u64_o(const aff_t<fp2p_t> a, uint64_t k) {
+  jac_t<fp2p_t> r = jac_from_aff(a);
+  int top = 63;
+  while (top > 0 && !((k >> top) & 1)) --top;
+  for (int i = top - 1; i >= 0; --i) {
+    r = jac_dbl_o(r);
+    if ((k >> i) & 1) r = jac_add_aff_q(r, a);
+  }
+  return r;
+}
+__device__ __noinline__ jac_t<fp2p_t> jac_mul_u64_jac_o(const jac_t<fp2p_t> p, uint64_t k) {
+  jac_t<fp2p_t> r = p;
+  int top = 63;
+  while (top > 0 && !((k >> top) & 1)) --top;
+  for (int i = top - 1; i >= 0; --i) {
+    r = jac_dbl_o(r);
+    if ((k >> i) & 1) r = jac_add_q(r, p);
+  }
+  return r;
+}
+
+// g2_mul_bp_q with the ladders' doublings on the octet
+__device__ __noinline__ jac_t<fp2p_t> g2_mul_bp_o(const aff_t<fp2p_t> p) {
+  aff_t<fp2p_t> np;
+  np.x = p.x;
+  np.y = fp2_neg(p.y);
+  const jac_t<fp2p_t> t1 = jac_mul_u64_o(p, BLS_X_ABS);                                   // [|x|]P
+  jac_t<fp2p_t> Q0 = jac_add_aff_q(jac_add_q(jac_mul_u64_jac_o(t1, BLS_X_ABS), t1), np);  // [x^2 - x - 1]P
+  Q0 = jac_add_q(Q0, g2_psi_jac_q(jac_add_aff_q(jac_neg(t1), np)));                      // + psi([x - 1]P)
+  return jac_add_q(Q0, g2_psi_jac_q(g2_psi_jac_q(jac_dbl_o(jac_from_aff(p)))));          // + psi^2(2P)
+}
+
 // fp6_mul_inl with its six Karatsuba products split A | B (the same formula, bit-identical)
 __device__ __forceinline__ fp6p_t fp6_mul_oct(const fp6p_t& s, const fp6p_t& t) {
   const bool b = oc_b();
