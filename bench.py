@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--secondary-timeout", type=int, default=360,
                     help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
-                    help="comma list: run only these secondary lines (deposits, randomized, c3, c4, c5, rccl, latency)")
+                    help="comma list: run only these secondary lines (host, deposits, randomized, c3, c4, c5, rccl, latency)")
     ap.add_argument("--rb-batch", type=str, default="32", help="randomized sub-batch sizes (comma list)")
     ap.add_argument("--c4-keys", type=int, default=1 << 17, help="pubkeys per GPU in the C4 aggregation")
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
@@ -224,28 +224,22 @@ PROFILE_KERNEL = {"decode_g1": "k_decode_g1", "decode_g2": "k_decode_g2", "decod
                   "final_exp_q": "k_final_exp_verdict_q<1>", "miller_loop_2q": "k_miller_verify_q"}
 # the C2 batch (2^16 items) runs the split Miller loop: the monolithic count is not part of its pipeline
 PIPELINE_STAGES = ["decode_g1", "decode_g2", "hash_to_g2", "miller_lines", "miller_accum", "final_exp"]
-# the final exponentiation of the throughput path runs as six launches (BLS_FE_SPLIT): its stage is
-# their sum; kernel symbols (PMC / rocprof names) with their launches per step
-FE_SPLIT_KEYS = ("final_exp_easy", "final_exp_pow", "final_exp_last")
-FE_SPLIT_KERNELS = [("k_fe_easy", 1), ("k_fe_pow<0>", 2), ("k_fe_pow<1>", 1), ("k_fe_pow<2>", 1), ("k_fe_last", 1)]
 
 
 def stage_times(prof, steps):
-    """ms per step of each pipeline stage from the profile (the split final exponentiation's six
-    launches summed into "final_exp")"""
-    ms = {k: v["total_ms"] / steps for k, v in prof.items() if k not in FE_SPLIT_KEYS}
+    """ms per step of each pipeline stage from the profile (the final exponentiation's exact pass
+    over its rare g2 = 0 waves, k_final_exp_redo, is part of the final_exp stage)"""
+    ms = {k: v["total_ms"] / steps for k, v in prof.items()}
     # the one-lane signature decode (profile key "decode_g2_1") is the C2 pipeline's decode_g2 stage
     if "decode_g2_1" in ms:
         ms["decode_g2"] = ms.pop("decode_g2_1") + ms.get("decode_g2", 0.0)
-    if any(k in prof for k in FE_SPLIT_KEYS):
-        ms["final_exp"] = sum(prof[k]["total_ms"] for k in FE_SPLIT_KEYS if k in prof) / steps
+    if "final_exp_redo" in ms:
+        ms["final_exp"] = ms.get("final_exp", 0.0) + ms.pop("final_exp_redo")
     return ms
 
 
 def stage_kernels(prof_key, prof):
     """[(kernel symbol, launches per step)] of a stage"""
-    if prof_key == "final_exp" and "final_exp_pow" in prof:
-        return FE_SPLIT_KERNELS
     if prof_key == "decode_g2" and "decode_g2_1" in prof:
         return [(PROFILE_KERNEL["decode_g2_1"], 1)]
     return [(PROFILE_KERNEL.get(prof_key, "k_" + prof_key), 1)]
@@ -797,6 +791,11 @@ def bench_native_comm(native, args, world, rank, dist, dev):
     out = {"n_gpus": world, "rccl": {"library": os.path.realpath(comm.rccl_path()),
                                      "mapped": comm.loaded_rccl_paths()}}
     out["rccl"]["single_copy"] = len(out["rccl"]["mapped"]) <= 1
+    # the communicator as the library sees it (bls381_comm_size / _rank): the sharded lines below run
+    # through it, not through torch.distributed
+    out["rccl"]["world"], out["rccl"]["rank"] = comm.size(), comm.rank()
+    if out["rccl"]["world"] != world:
+        raise RuntimeError("library communicator has %d ranks, expected %d" % (out["rccl"]["world"], world))
     try:
         k = args.c4_keys * world
         base = native.privtopub_batch(b"".join(j.to_bytes(32, "big") for j in range(1, 65)))
@@ -1169,7 +1168,8 @@ def main():
     # waiting in it, so any error ends the phase, and a watchdog on every rank ends it after
     # --secondary-timeout s: rank 0 prints the headline with the lines that finished, every rank
     # exits 0 (3 with --fail-on-secondary-error, which tools/gpu_final.sh passes).
-    sec = {"other_policy": None, "cpu_baseline": None, "cpu_baseline_cpp": None, "aggregation": None}
+    sec = {"c2_host_buffers": None, "other_policy": None, "cpu_baseline": None, "cpu_baseline_cpp": None,
+           "aggregation": None}
     import threading
     state = {"printed": False}
     emit_lock = threading.Lock()
@@ -1207,8 +1207,26 @@ def main():
                 stop_phase(msg)
             sec[key] = {"error": msg}
 
+    def bench_host_buffers():
+        # the same C2 batch through the host-buffer entry point (bls381_verify_batch: 184 B per item
+        # copied in over PCIe, verdicts copied out, both inside the time) beside the device-resident
+        # headline
+        native.verify_batch(pks, msgs, sigs, doms)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            got = native.verify_batch(pks, msgs, sigs, doms)
+        ht = _max_time(time.perf_counter() - t0, world, dist, dev)
+        assert np.array_equal(got, expected), "host-buffer verdict mismatch"
+        return {"entry_point": "bls381_verify_batch (host buffers in, verdicts out)",
+                "verifications_per_s": n * args.steps * world / ht, "ms_per_step": 1e3 * ht / args.steps,
+                "bytes_in_per_step": 184 * n, "bytes_out_per_step": n}
+
     only = set(x for x in args.sections.split(",") if x)
     want = lambda k: (not args.no_secondary and not only) or k in only
+    if want("host"):
+        guarded("c2_host_buffers", bench_host_buffers)
     if not args.no_secondary:
         guarded("other_policy", bench_other_policy)
     if not args.no_aggregate:

@@ -30,6 +30,11 @@ Divergences from that contract (tested in tests/test_gpu_parity.py):
   bls_verify_multiple and bls_sign, where py_ecc would hash it and return a verdict.
   The spec's message_hash is Bytes32, so no spec call reaches the limit; raising
   keeps a verdict from ever being guessed for an input the engine did not hash.
+* bls_verify_multiple with a domain outside [0, 2^64) and an undecodable pubkey in one
+  of several message groups: py_ecc 1.7.0 walks set(message_hashes), so whether it
+  decodes that group first (False) or serialises the domain first (OverflowError)
+  depends on the process's hash seed.  This module takes the sorted order; the
+  fixtures mark both cases as order-dependent (pyecc_order_dependent).
 Messages up to the limit may have any length, and one bls_verify_multiple call may
 mix lengths (each length group becomes a partial Miller product; one final
 exponentiation decides the call).

@@ -84,7 +84,7 @@ SANITIZE_DIR = os.environ.get("BLS381_SANITIZE_DIR", os.path.expanduser("~/.cach
 
 
 def build_hostcheck(force=False, sanitize=False, count_ops=False, defines=()):
-    """defines: build-knob variants (e.g. ("BLS_ML_LINE_PAIR=1",)) -- test-only, built out of
+    """defines: build-knob variants (e.g. ("BLS_WAVES_PER_EU=1",)) -- test-only, built out of
     tree like the sanitized library."""
     os.makedirs(LIB, exist_ok=True)
     name = "libbls381_hostcheck_asan.so" if sanitize else (

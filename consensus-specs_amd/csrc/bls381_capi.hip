@@ -213,64 +213,39 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
 // final exponentiation + verdict of n Fp12 values (lane-pair SoA): on lane quads while
 // the batch leaves SIMDs idle (k_final_exp_verdict_q: half the per-item latency, more
 // lane work), on lane pairs above that
-// BLS_ML_ACCUM_QUAD=1 (measurement knob): the throughput path's f accumulation on lane quads
-// (k_ml_accum_q: each lane holds half of f, 42 words instead of 84) instead of lane pairs
-#ifndef BLS_ML_ACCUM_QUAD
-#define BLS_ML_ACCUM_QUAD 0
-#endif
 #ifndef BLS_FE_QUAD_MAX_N
 #define BLS_FE_QUAD_MAX_N 49152
 #endif
-// final exponentiations of at most this many values run on lane octets (k_final_exp_verdict_o:
-// the squarings split four ways) -- BLS381_FE_OCT=0 keeps them on quads (measurement knob)
+// final exponentiations of at most this many values run on lane octets (k_final_exp_verdict_oq)
+// -- BLS381_FE_OCT=0 keeps them on quads (measurement knob)
 #ifndef BLS_FE_OCT_MAX_N
 #define BLS_FE_OCT_MAX_N 8192
 #endif
 int env_knob(const char* name, int def);
-// BLS381_FE_OCT: 0 = quads (k_final_exp_verdict_q), 1 = octets with the squarings split four ways
-// (k_final_exp_verdict_o), 2 = octets with the Fp12 products split (k_final_exp_verdict_oq<.., 0>),
-// 3 (default) = both (k_final_exp_verdict_oq<.., 1>)
+// BLS381_FE_OCT: 0 = quads (k_final_exp_verdict_q), 2 = octets with the Fp12 products split
+// (k_final_exp_verdict_oq<.., 0>), 3 (default) = the compressed squarings split four ways as well
+// (k_final_exp_verdict_oq<.., 1>).  (1, the squarings split without the products, measured
+// slower than 2 and was removed in r06.)
 int fe_oct_mode() {
   static const int m = env_knob("BLS381_FE_OCT", 3);
   return m;
 }
 bool fe_oct(size_t n) { return fe_oct_mode() && n <= BLS_FE_OCT_MAX_N; }
-// BLS_FE_SPLIT=1 (measurement knob): the throughput-path final exponentiation as six launches
-// (k_fe_easy, k_fe_pow, k_fe_last) over 4 Fp12 buffers per item (fe_ws_words); 0 (default): the
-// one-kernel k_final_exp_verdict.  r04d: 9.99 ms per 2^16 step split against ~9.1 in one kernel --
-// each launch still carries cyc_exp_x's frame, and its own product frame (fe_pow_run 2.4 KB)
-// is as large as the values it no longer keeps.
-#ifndef BLS_FE_SPLIT
-#define BLS_FE_SPLIT 0
-#endif
-size_t fe_ws_words(size_t n) { return (BLS_FE_SPLIT && n > BLS_FE_QUAD_MAX_N) ? 4 * 12 * FP_LIMBS * n : 0; }
-
-// tmp: fe_ws_words(n) words for the split form (nullptr: the one-kernel form)
-int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts,
-                     uint32_t* tmp = nullptr) {
-  if (tmp && fe_ws_words(n)) {
-    const dim3 g(grid_for(2 * n)), b(KBLOCK);
-    const size_t one = 12 * FP_LIMBS * n;   // one Fp12 per item, pair SoA
-    uint32_t *T = tmp, *A = tmp + one, *A2 = tmp + 2 * one, *B = tmp + 3 * one;
-    LAUNCH("final_exp_easy", s, g, b, k_fe_easy, n, f, st, T);
-    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_CONJ>, n, (const uint32_t*)T, st, A);
-    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_CONJ>, n, (const uint32_t*)A, st, A2);
-    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_FROB1>, n, (const uint32_t*)A2, st, B);
-    LAUNCH("final_exp_pow", s, g, b, k_fe_pow<FE_NONE>, n, (const uint32_t*)B, st, A);
-    LAUNCH("final_exp_last", s, g, b, k_fe_last, n, (const uint32_t*)A, (const uint32_t*)B, (const uint32_t*)T, st,
-           verdicts);
-    return 0;
-  }
+// The throughput form is k_final_exp_verdict followed by k_final_exp_redo (the exact pass over
+// the items whose wave met the compressed squarings' g2 = 0 case; a wave with none exits at once).
+// (r04d measured the throughput FE as six launches with HBM intermediates, BLS_FE_SPLIT: 9.99 ms
+// per 2^16 against ~9.1 in one kernel; removed in r06)
+int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* st, uint8_t* verdicts) {
   if (fe_oct(n) && fe_oct_mode() == 3)
     LAUNCH("final_exp_oo", s, dim3(grid_for(8 * n)), dim3(KBLOCK), (k_final_exp_verdict_oq<1, 1>), n, f, st, verdicts);
   else if (fe_oct(n) && fe_oct_mode() == 2)
     LAUNCH("final_exp_oq", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_oq<1>, n, f, st, verdicts);
-  else if (fe_oct(n))
-    LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), dim3(KBLOCK), k_final_exp_verdict_o<1>, n, f, st, verdicts);
   else if (n <= BLS_FE_QUAD_MAX_N)
     LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), dim3(KBLOCK), k_final_exp_verdict_q<1>, n, f, st, verdicts);
-  else
+  else {
     LAUNCH("final_exp", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_final_exp_verdict, n, f, st, verdicts);
+    LAUNCH("final_exp_redo", s, dim3(grid_for(2 * n)), dim3(KBLOCK), k_final_exp_redo, n, f, verdicts);
+  }
   return 0;
 }
 #define LAUNCH_FE(s, n, f, st, v)                                                                   \
@@ -281,7 +256,7 @@ int launch_final_exp(hipStream_t s, size_t n, const uint32_t* f, const uint8_t* 
 
 // ----------------------------------------------------- verify_batch (C2) --
 struct VerifyWs {
-  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff, *ml_L, *fe_tmp;
+  uint32_t *pk_aff, *sig_aff, *h_aff, *f, *koff, *ml_L;
   uint8_t *pk_st, *sig_st, *f_st, *ml_st;
 };
 // bls_verify batches of at most this many items run each Miller pair on its own lane
@@ -313,8 +288,7 @@ size_t verify_split_chunk(size_t n) { return verify_split(n) ? std::min<size_t>(
 size_t verify_ws_size(size_t n, bool lines = true) {
   const size_t ch = lines ? verify_split_chunk(n) : 0;
   return align256(2 * FPW * n) + align256(4 * FPW * n) * 2 + align256(12 * FPW * verify_nf(n)) + 2 * align256(n) +
-         align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) +
-         (lines ? align256(4 * fe_ws_words(n)) : 0) + 1024;
+         align256(verify_nf(n)) + align256(4 * n) + align256(4 * ML_L_WORDS_PER_ITEM * ch) + align256(ch) + 1024;
 }
 VerifyWs carve_verify(void* ws, size_t n, bool lines = true) {
   Bump b(ws);
@@ -330,7 +304,6 @@ VerifyWs carve_verify(void* ws, size_t n, bool lines = true) {
   w.sig_st = b.take<uint8_t>(n);
   w.f_st = b.take<uint8_t>(verify_nf(n));
   w.koff = b.take<uint32_t>(n);
-  w.fe_tmp = lines && fe_ws_words(n) ? b.take<uint32_t>(fe_ws_words(n)) : nullptr;
   return w;
 }
 
@@ -350,9 +323,10 @@ bool verify_split(size_t n) { return BLS_ML_SPLIT && n > BLS_ML_QUAD_MAX_N; }
 #define BLS_DECODE_G2_SIDE 1
 #endif
 // A/B knobs read once from the environment (measurement only; defaults are the shipped
-// layout): BLS381_G2_ONE_LANE bit 0 = decode_g2, bit 1 = hash_to_g2 on one lane per item.
-// Default 1 (r03k, same box, two runs each): the one-lane decode_g2 beside hash_to_G2 runs
-// 4.1 -> 3.45 ms, C2 2.116 -> 2.133-2.139 M/s; the one-lane hash spills (10 ms against 6.6).
+// layout): BLS381_G2_ONE_LANE bit 0 = decode_g2 on one lane per item.  Default 1 (r03k, same
+// box, two runs each): the one-lane decode_g2 beside hash_to_G2 runs 4.1 -> 3.45 ms, C2 2.116 ->
+// 2.133-2.139 M/s.  (Bit 1, the whole hash_to_g2 on one lane, spilled -- 10 ms against 6.6 --
+// and was removed in r06.)
 int env_knob(const char* name, int def) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : def;
@@ -466,9 +440,7 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   const bool wide = n <= BLS_HASH_WIDE_MAX_N;
   if (wide)
     LAUNCH("hash_search", s, dim3(grid_for(16 * n)), b, k_hash_search<16>, n, msgs, (uint32_t)32, doms, 8, w.koff);
-  if (!wide && (g2_one_lane() & 2))
-    LAUNCH("hash_to_g2", s, g, b, k_hash_g2_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff, (uint8_t*)nullptr);
-  else if (!wide && (c2_order == 3 || c2_order == 4) && hash_split()) {
+  if (!wide && (c2_order == 3 || c2_order == 4) && hash_split()) {
     LAUNCH("hash_cand", s, g, b, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
     HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
     if (c2_order == 4 && (g2_one_lane() & 1)) HIPC(hipStreamWaitEvent(s, c->ev_join2, 0));
@@ -508,9 +480,6 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
     else if (fe_oct(n) && fe_oct_mode() == 2)
       LAUNCH("final_exp_oq", s, dim3(grid_for(8 * n)), b, k_final_exp_verdict_oq<2>, n, (const uint32_t*)w.f,
              (const uint8_t*)w.f_st, verdicts);
-    else if (fe_oct(n))
-      LAUNCH("final_exp_o", s, dim3(grid_for(8 * n)), b, k_final_exp_verdict_o<2>, n, (const uint32_t*)w.f,
-             (const uint8_t*)w.f_st, verdicts);
     else
       LAUNCH("final_exp_q", s, dim3(grid_for(4 * n)), b, k_final_exp_verdict_q<2>, n, (const uint32_t*)w.f,
              (const uint8_t*)w.f_st, verdicts);
@@ -531,20 +500,16 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
       LAUNCH("miller_lines", s, dim3(grid_for(4 * cnt)), b, k_ml_lines, n, i0, cnt, (const uint32_t*)w.sig_aff,
              (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
              w.ml_L, w.ml_st, sig_in_loop ? 1 : 0);
-#if BLS_ML_ACCUM_QUAD
-      LAUNCH("miller_accum", s, dim3(grid_for(4 * cnt)), b, k_ml_accum_q, n, i0, cnt, (const uint32_t*)w.ml_L,
-             (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);
-#else
+      // (r05: the accumulation on lane quads, k_ml_accum_q, measured 8.09-8.18 against 6.96-7.00 ms)
       LAUNCH("miller_accum", s, dim3(grid_for(2 * cnt)), b, k_ml_accum, n, i0, cnt, (const uint32_t*)w.ml_L,
              (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);
-#endif
     }
   } else {
     LAUNCH("miller_loop_2", s, g2, b, k_miller_verify, n, (const uint32_t*)w.sig_aff, (const uint8_t*)w.sig_st,
            (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff, w.f, w.f_st,
            sig_in_loop ? 1 : 0);
   }
-  if (int rc = launch_final_exp(s, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts, w.fe_tmp)) return rc;
+  if (int rc = launch_final_exp(s, n, (const uint32_t*)w.f, (const uint8_t*)w.f_st, verdicts)) return rc;
   return 0;
 }
 
@@ -2552,7 +2517,11 @@ int bls381_comm_rank(void) {
 
 void bls381_comm_destroy(void) {
   std::lock_guard<std::mutex> lk(g_comm_mu);
+  // the device-resident sharded calls return with their collectives still queued on the
+  // caller's stream (rows_ev is recorded after the last one): the communicator must outlive them
+  if (g_comm.rows_ev) (void)hipEventSynchronize(g_comm.rows_ev);
   if (g_comm.comm) {
+    (void)hipDeviceSynchronize();
     RcclApi* api = rccl_api();
     if (api) (void)api->comm_destroy(g_comm.comm);
   }
@@ -2757,6 +2726,7 @@ static int agg_sharded_impl(Ctx* c, Comm* cm, RcclApi* api, size_t n_local, cons
     uint32_t* row = (uint32_t*)(cm->virt ? d_rows + row_b * rr : d_rows + row_b * R);
     const size_t lo = cm->virt ? rr * base + (rr < extra ? rr : extra) : 0;
     const size_t cnt = cm->virt ? base + (rr < extra ? 1 : 0) : n_local;
+    // force_err: the caller could not stage its keys (d_workspace may be null): a flagged row only
     const int lrc = force_err ? force_err : local_stage([&]() -> int {
       const uint32_t off1[2] = {0, (uint32_t)cnt};
       auto hold = std::make_shared<AggPlan>(plan_agg(1, off1, 1));
@@ -2849,8 +2819,9 @@ int bls381_aggregate_pubkeys_sharded(size_t n, const uint8_t* pks, uint8_t out[4
     d_in = d_pks;
   }
   // a rank that cannot stage its keys still issues every collective of the call, with a flagged row
+  // (with force_err set the impl runs no local stage, so it never touches the workspace)
   rc = agg_sharded_impl(c, cm, api, local ? 0 : cnt, local ? nullptr : d_in, d_res, (int32_t*)(d_res + 48),
-                        local ? (void*)(d_res - 16384) : w, s, local);
+                        local ? nullptr : w, s, local);
   int32_t st = 0;
   HIPC(hipMemcpyAsync(out, d_res, 48, hipMemcpyDeviceToHost, s));
   HIPC(hipMemcpyAsync(&st, d_res + 48, 4, hipMemcpyDeviceToHost, s));
@@ -2990,37 +2961,36 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   uint8_t* s_st = b.take<uint8_t>(nb);
   {
     // Order, BLS381_RB_ORDER (measurement knob):
-    //  0 (default): everything in sequence on the main stream, except the sub-batch sums'
-    //    latency-bound Miller loops (high-priority stream, beside hash_to_G2).
-    //  1: hash_to_G2 on the main stream, the signature branch (decode_g1, decode_g2,
-    //    [r_i] sig_i, the sums) and [r_i] pk_i beside it on the side stream: measured r03j,
-    //    30.3 against 28.1 ms per clean 2^16 batch (two different large kernels co-resident).
+    //  2 (default, r06): the default path's order-4 prologue -- k_rb_decode_g1 (decode + [r_i] pk_i)
+    //    on the side stream, the codec-only k_decode_g2_1 on the second side stream and the
+    //    hash's one-lane k_hash_cand_1 on the main stream share the chip; then the signatures' G2
+    //    test + item classes (k_rb_g2_test, lane pairs) and the signature sums; the sums' Miller
+    //    loops on the high-priority stream beside k_hash_bp, then the item Miller loops.
+    //  0 (round 5): decode_g1, decode_g2 with the G2 test (pairs) and the signature sums in
+    //    sequence on the main stream, the sums' Miller loops on the high-priority stream beside
+    //    hash_to_G2 (pair kernel) and [r_i] pk_i (k_rb_scale_g1).
     std::lock_guard<std::mutex> lk(c->fork_mu);
-    static const int order = env_knob("BLS381_RB_ORDER", 0);
+    static const int order = env_knob("BLS381_RB_ORDER", 2);
     hipStream_t sb = s;
-    if (order == 1) {
-      sb = c->side;
-      HIPC(hipEventRecord(c->ev_fork, s));
-      HIPC(hipStreamWaitEvent(sb, c->ev_fork, 0));
-      LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
-             (const uint32_t*)nullptr, 0);
-    }
-    // BLS381_RB_HASH (measurement knob, order 0 only): 0 = the pair kernel k_hash_g2 in sequence;
-    // 1 = the one-lane candidate search + root (k_hash_cand_1) on the side stream beside
-    // decode_g1 (two one-lane launches of 2^16 items fill two waves per SIMD together), the
-    // cofactor map (k_hash_bp) in sequence
-    // 2 = the split hash (k_hash_cand_1, k_hash_bp) in sequence where the pair kernel runs
-    static const int rb_hash = env_knob("BLS381_RB_HASH", 0);
-    const bool hash_side = order != 1 && rb_hash == 1;
-    if (hash_side) {
+    if (order == 2) {
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      LAUNCH("hash_cand", c->side, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
-      HIPC(hipEventRecord(c->ev_join3, c->side));
+      HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
+      LAUNCH("rb_decode_g1", c->side, g1, blk, k_rb_decode_g1, n, pks, (const uint8_t*)d_seed, w.pk_aff, w.pk_st, r1,
+             r1_st, policy_flags(chk));
+      HIPC(hipEventRecord(c->ev_join, c->side));
+      LAUNCH("decode_g2_1", c->side2, g1, blk, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, policy_flags(0));
+      HIPC(hipEventRecord(c->ev_join3, c->side2));
+      LAUNCH("hash_cand", s, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
+      HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+      HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
+      LAUNCH("rb_g2_test", s, g2, blk, k_rb_g2_test, n, (const uint32_t*)w.sig_aff, w.sig_st, (const uint8_t*)w.pk_st,
+             cls, chk);
+    } else {
+      LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
+      // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
+      LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
     }
-    LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
-    // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-    LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
     // BLS381_RB_MSM (measurement knob): 1 (default) the sub-batch sums sum_i [r_i] sig_i as one bucket
     // MSM per sub-batch (k_rb_msm_*); 0 a joint 32-bit ladder per item (k_rb_scale_g2) and a tree sum
     // The MSM gives each (sub-batch, window, digit) bucket to one lane pair, which adds its ~B/16
@@ -3061,21 +3031,14 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
-    if (hash_side) {
-      HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
+    if (order == 2) {
+      // the cofactor map beside the sums' Miller loops (which raise their waves' priority)
       LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
-    } else if (order != 1 && rb_hash == 2) {
-      LAUNCH("hash_cand", s, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
-      LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
-    } else if (order != 1) {
+    } else {
       LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
              (const uint32_t*)nullptr, 0);
-    }
-    LAUNCH("rb_scale_g1", sb, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
-           (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
-    if (order == 1) {
-      HIPC(hipEventRecord(c->ev_join, sb));
-      HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
+      LAUNCH("rb_scale_g1", sb, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
+             (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
     }
     // the batched items two per Miller accumulator: lines of both pairs on a quad, then f^2 L
     // on quads (2^15 accumulators per 2^16 items: a pair launch would leave SIMDs half empty)

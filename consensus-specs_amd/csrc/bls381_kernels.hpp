@@ -263,21 +263,6 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t
   st[i] = (uint8_t)s;
   if (s == PT_OK || s == ST_NOSUB) soa_st_g2_1(out, n, i, a);
 }
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_g2_1(size_t n, const uint8_t* __restrict__ msgs,
-                                                     uint32_t mlen, const uint8_t* __restrict__ doms,
-                                                     int dom_stride, uint32_t* __restrict__ out,
-                                                     uint8_t* __restrict__ st) {
-  const size_t i = item_index<1>();
-  if (i >= n) return;
-  uint8_t dom[8];
-  ld_bytes(dom, doms + (size_t)dom_stride * i, 8);
-  aff_t<fp2_t> c;
-  hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
-  aff_t<fp2_t> h;
-  const bool fin = jac_to_aff(h, g2_mul_bp(c));
-  if (st) st[i] = fin ? ST_OK : ST_INF;
-  if (fin) soa_st_g2_1(out, n, i, h);
-}
 
 // hash_to_G2 in two launches (the throughput path): the try-and-increment search and the
 // square root on one lane per item (k_hash_cand_1: the root's two Fp exponentiations once
@@ -1019,6 +1004,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_miller_verify_o
   if (lead) st_out[t] = degen ? ST_BAD : ST_OK;
 }
 
+// The throughput final exponentiation (lane pairs).  It runs cyc_exp_x without its exact
+// fallback (final_exp_check<.., 0>): the items of a wave that met a snapshot with g2 = 0 get
+// verdict FE_REDO, and k_final_exp_redo, queued right behind it, recomputes exactly those with
+// the fallback in its call tree.  Nothing reads the verdicts between the two launches.
+constexpr uint8_t FE_REDO = 0xFF;
 __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict(size_t n, const uint32_t* __restrict__ f_in,
                                                              const uint8_t* __restrict__ st,
                                                              uint8_t* __restrict__ verdict) {
@@ -1027,83 +1017,19 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   const bool lead = !pr_odd();
   if (st[i] != ST_OK) { if (lead) verdict[i] = 0; return; }
   const fp12p_t f = soa_ld12(f_in, n, i);
-  const bool one = fp12_is_one(final_exp(f));
-  if (lead) verdict[i] = one ? 1 : 0;
+  const int v = final_exp_check<fp2p_t, 0>(f);
+  if (lead) verdict[i] = v == 2 ? FE_REDO : (uint8_t)v;
 }
 
-// ---- the final exponentiation as six launches (the throughput path, BLS_FE_SPLIT) ----
-// f^(3(q^12-1)/r) = easy part, then the hard part (x-1)^2 (x+q) (x^2+q^2-1) + 3 of final_exp
-// (bls381_pairing.hpp), one exponentiation by x per launch with the products next to it:
-//   k_fe_easy              t = f^((q^6-1)(q^2+1))                       -> T
-//   k_fe_pow<FE_CONJ> x2   a = cyc_exp_x(u) conj(u): T -> A, A -> A2
-//   k_fe_pow<FE_FROB1>     b = cyc_exp_x(a) frob(a)                       A2 -> B
-//   k_fe_pow<FE_NONE>      y = cyc_exp_x(b)                               B -> A
-//   k_fe_last              cyc_exp_x(y) frob^2(b) conj(b) t^3 == 1        -> verdict
-// The values the chain needs again later (t, b, the launch's own input) wait in HBM as pair
-// SoA, coalesced, instead of living across the exponentiation calls of one long kernel (in
-// its scratch frame: 7.2 KB/lane and ~10 GB of spill traffic per 2^16 launch, r04b).
-enum : int { FE_CONJ = 0, FE_FROB1 = 1, FE_NONE = 2 };
-
-// Each launch's work is one non-inlined device function: its temporaries (the Fp12 values
-// handed by reference to cyc_exp_x and the products) live in a stack-pointer-relative frame.
-// (Written inline in the kernels, hipcc 7.2 stops with "Illegal instruction detected: Operand
-// has incorrect register class: V_CMP_NE_U32_e32 0, $src_private_base" -- a private-to-flat
-// pointer check on a kernel frame object.)
-__device__ __noinline__ void fe_easy_run(size_t n, size_t i, const uint32_t* __restrict__ f_in,
-                                         uint32_t* __restrict__ t_out) {
-  const fp12p_t f = soa_ld12(f_in, n, i);
-  fp12p_t t = fp12_mul_inl(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
-  t = fp12_mul_inl(fp12_frob(t, 2), t);                    // ^(q^2 + 1)
-  soa_st12(t_out, n, i, t);
-}
-
-template <int MODE>
-__device__ __noinline__ void fe_pow_run(size_t n, size_t i, const uint32_t* __restrict__ u_in,
-                                        uint32_t* __restrict__ w_out) {
-  fp12p_t w = cyc_exp_x(soa_ld12(u_in, n, i));
-  if (MODE != FE_NONE) {
-    const fp12p_t u = soa_ld12(u_in, n, i);               // re-read, not kept across the call
-    w = fp12_mul_inl(w, MODE == FE_CONJ ? fp12_conj(u) : fp12_frob(u, 1));
-  }
-  soa_st12(w_out, n, i, w);
-}
-
-__device__ __noinline__ bool fe_last_run(size_t n, size_t i, const uint32_t* __restrict__ y_in,
-                                         const uint32_t* __restrict__ b_in, const uint32_t* __restrict__ t_in) {
-  fp12p_t c = cyc_exp_x(soa_ld12(y_in, n, i));                                // b^(x^2)
-  {
-    const fp12p_t b = soa_ld12(b_in, n, i);
-    c = fp12_mul_inl(fp12_mul_inl(c, fp12_frob(b, 2)), fp12_conj(b));      // b^(x^2 + q^2 - 1)
-  }
-  const fp12p_t t = soa_ld12(t_in, n, i);
-  return fp12_is_one(fp12_mul_inl(c, fp12_mul_inl(fp12_cyclotomic_sqr(t), t)));
-}
-
-__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_easy(size_t n, const uint32_t* __restrict__ f_in,
-                                                     const uint8_t* __restrict__ st, uint32_t* __restrict__ t_out) {
+// the exact pass over k_final_exp_verdict's FE_REDO items (a wave without one exits at once)
+__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_redo(size_t n, const uint32_t* __restrict__ f_in,
+                                                          uint8_t* __restrict__ verdict) {
   const size_t i = item_index<2>();
-  if (i >= n || st[i] != ST_OK) return;
-  fe_easy_run(n, i, f_in, t_out);
-}
-
-template <int MODE>
-__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_pow(size_t n, const uint32_t* __restrict__ u_in,
-                                                    const uint8_t* __restrict__ st, uint32_t* __restrict__ w_out) {
-  const size_t i = item_index<2>();
-  if (i >= n || st[i] != ST_OK) return;
-  fe_pow_run<MODE>(n, i, u_in, w_out);
-}
-
-__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_fe_last(size_t n, const uint32_t* __restrict__ y_in,
-                                                     const uint32_t* __restrict__ b_in,
-                                                     const uint32_t* __restrict__ t_in,
-                                                     const uint8_t* __restrict__ st, uint8_t* __restrict__ verdict) {
-  const size_t i = item_index<2>();
-  if (i >= n) return;
+  if (i >= n || verdict[i] != FE_REDO) return;
   const bool lead = !pr_odd();
-  if (st[i] != ST_OK) { if (lead) verdict[i] = 0; return; }
-  const bool one = fe_last_run(n, i, y_in, b_in, t_in);
-  if (lead) verdict[i] = one ? 1 : 0;
+  const fp12p_t f = soa_ld12(f_in, n, i);
+  const int v = final_exp_check<fp2p_t, 1>(f);
+  if (lead) verdict[i] = (uint8_t)v;
 }
 
 // The same verdict on a lane quad (final_exp_q: each half holds one Fp6 half of
@@ -1168,34 +1094,6 @@ __global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdi
   if (lead) verdict[i] = one ? 1 : 0;
 }
 
-// The octet form (final_exp_o, 8 lanes per item) of k_final_exp_verdict_q: the lowest
-// latency, for single calls and small batches (BLS381_FE_OCT=1; off by default until measured).
-template <int NF>
-__global__ void __launch_bounds__(KBLOCK, BLS_FE_WAVES_PER_EU) k_final_exp_verdict_o(size_t n, const uint32_t* __restrict__ f_in,
-                                                               const uint8_t* __restrict__ st,
-                                                               uint8_t* __restrict__ verdict) {
-  size_t i;
-  bool live;
-  if (!lat_unit<8>(n, i, live)) return;
-  const bool lead = (threadIdx.x & 7u) == 0 && live;
-  bool ok = true;
-  for (int k = 0; k < NF; ++k) ok = ok && st[NF * i + k] == ST_OK;
-  if (!ok) { if (lead) verdict[i] = 0; return; }
-  const int p = pr_odd() ? 1 : 0;
-  const int c0 = qd_hi() ? 3 : 0;
-  const size_t nv = NF * n;
-  auto load = [&](size_t v) {
-    fq12_t g;
-    g.h.c0 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 0));
-    g.h.c1 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 1));
-    g.h.c2 = pr_make(soa_ld(f_in, 2 * nv, 2 * v + p, c0 + 2));
-    return g;
-  };
-  fq12_t f = load(NF * i);
-  for (int k = 1; k < NF; ++k) f = fq12_mul(f, load(NF * i + k));
-  const bool one = fq12_is_one(final_exp_o(f));
-  if (lead) verdict[i] = one ? 1 : 0;
-}
 
 // ------------------------------------- randomized batch verification (opt-in) --
 // Small-exponent batch test (SURVEY.md §7 "Verdict semantics under batching"):
@@ -1253,6 +1151,58 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t
     }
   }
   r1_st[i] = st;
+}
+
+// The randomized prologue (round 6), in the default path's order-4 shape: three one-lane
+// launches share the chip -- k_rb_decode_g1 (decode + [r_i] pk_i), k_decode_g2_1 (codec only)
+// and the hash's k_hash_cand_1 -- then the pair launches k_hash_bp and k_rb_g2_test.
+// k_rb_decode_g1: one lane per item; the pubkey decoded under the call's codec and subgroup mode
+// (as k_decode_g1), and for a finite key R1 = [r_i] pk_i affine (status OK / INF).  The class waits
+// for the signature's G2 test (k_rb_g2_test).
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_t n, const uint8_t* __restrict__ pks,
+                                                        const uint8_t* __restrict__ seed32,
+                                                        uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st,
+                                                        uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
+                                                        int check_subgroup) {
+  const size_t i = item_index<1>();
+  if (i >= n) return;
+  uint8_t b[48];
+  ld_bytes(b, pks + 48 * i, 48);
+  aff_t<fp_t> p;
+  int s = g1_decompress(p, b, (check_subgroup & CHK_LAX) != 0);
+  if (s == PT_OK && (check_subgroup & CHK_SUB_MASK) && !g1_in_subgroup(p)) s = PT_BAD;
+  pk_st[i] = (uint8_t)s;
+  uint8_t st = ST_INF;
+  if (s == PT_OK) {
+    soa_st_g1(pk_aff, n, i, p);
+    aff_t<fp_t> sp;                       // sigma(p) = [-x^2] p
+    sp.x = fp_mul(G1_BETA_M, p.x);
+    sp.y = p.y;
+    const rb_weight w = rb_scalar(seed32, i);
+    aff_t<fp_t> a;
+    if (jac_to_aff(a, jac_mul_2x32(p, sp, w.k0, w.k1))) {
+      soa_st_g1(r1_aff, n, i, a);
+      st = ST_OK;
+    }
+  }
+  r1_st[i] = st;
+}
+
+// k_rb_g2_test: one lane pair per item; the signature's G2 membership (psi(Q) == [x] Q) after the
+// one-lane codec-only decode, and the item's class: outside G2 the signature is ST_BAD (strict) or
+// ST_NOSUB (py_ecc: the item goes to the per-item path, where it is an ordinary point).
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_g2_test(size_t n, const uint32_t* __restrict__ sig_aff,
+                                                      uint8_t* __restrict__ sig_st,
+                                                      const uint8_t* __restrict__ pk_st,
+                                                      uint8_t* __restrict__ cls, int strict) {
+  const size_t i = item_index<2>();
+  if (i >= n) return;
+  uint8_t ss = sig_st[i];
+  if (ss == ST_OK && !g2_in_subgroup(soa_ld_g2(sig_aff, n, i))) ss = strict ? ST_BAD : ST_NOSUB;
+  if (pr_odd()) return;
+  const uint8_t ps = pk_st[i];
+  sig_st[i] = ss;
+  cls[i] = (ps == ST_BAD || ss == ST_BAD) ? RB_BAD : (ss == ST_NOSUB ? RB_SINGLE : RB_BATCH);
 }
 
 // per item, one lane pair: R2 = [r_i] sig_i (Jacobian SoA; infinity when the item is not
@@ -1465,6 +1415,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(s
                                                          const uint32_t* __restrict__ s_aff,
                                                          const uint8_t* __restrict__ s_st, size_t nslots,
                                                          uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
+  // a few latency-bound waves beside a full-chip launch (k_hash_bp): they win their SIMD's issue
+  // arbitration, so the sums' loops end before the item Miller loops need every wave slot
+  __builtin_amdgcn_s_setprio(3);
   const size_t b = item_index<4>();
   if (b >= nb) return;
   const size_t slot = b * (slot_per + 1) + slot_per;

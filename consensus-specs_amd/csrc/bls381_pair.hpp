@@ -123,15 +123,11 @@ __device__ __forceinline__ fp_t fp2p_sqr_body(const fp_t& a) {
   return fp_mul_body(x, y);
 }
 
-// BLS_FP2_INLINE=1 inlines the Fp2 product bodies everywhere (experiment knob)
-#ifndef BLS_FP2_INLINE
-#define BLS_FP2_INLINE 0
-#endif
-#if BLS_FP2_INLINE
-#define BLS_FP2_CALL __device__ __forceinline__
-#else
+// The lane-pair Fp2 products are calls (operands and result in VGPRs, no frame): inlining them
+// everywhere (round 2's BLS_FP2_INLINE=1) grew the callers' live sets, Miller 14.7-15.0 -> 16.9 ms;
+// round 5's scheduling-fenced inlined form (BLS_FP2_INLINE=2) faulted.
+// Both knobs were removed in round 6.
 #define BLS_FP2_CALL __device__ __attribute__((noinline))
-#endif
 BLS_FP2_CALL fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
   return fp_pack(fp2p_mul_body(fp_unpack(a), fp_unpack(b)));
 }
@@ -150,16 +146,7 @@ __device__ __forceinline__ fp2p_t fp2_neg(const fp2p_t& a) { return pr_make(fp_n
 __device__ __forceinline__ fp2p_t fp2_dbl(const fp2p_t& a) { return pr_make(fp_dbl(a.v)); }
 __device__ __forceinline__ fp2p_t fp2_half(const fp2p_t& a) { return pr_make(fp_half(a.v)); }
 __device__ __forceinline__ fp2p_t fp2_add_lazy(const fp2p_t& a, const fp2p_t& b) { return pr_make(fp_add_lazy(a.v, b.v)); }
-#if BLS_FP2_INLINE == 2
-__device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) {
-  BLS_PHASE();
-  const fp_t r = fp_mul_body(a.v, s);
-  BLS_PHASE();
-  return pr_make(r);
-}
-#else
 __device__ __forceinline__ fp2p_t fp2_mul_fp(const fp2p_t& a, const fp_t& s) { return pr_make(fp_mul(a.v, s)); }
-#endif
 __device__ __forceinline__ fp2p_t fp2_mul_small(const fp2p_t& a, int k) { return pr_make(fp_mul_small(a.v, k)); }
 __device__ __forceinline__ fp2p_t fp2_conj(const fp2p_t& a) { return pr_make(fp_sel(pr_odd(), fp_neg(a.v), a.v)); }
 // xi = 1 + u:  (a0 - a1) + (a0 + a1) u -- lane 0: a0 + (2q - a1), lane 1: a1 + a0
@@ -188,27 +175,10 @@ __device__ __forceinline__ fp2p_t fp2_3p2(const fp2p_t& X, const fp2p_t& x) { re
 __device__ __forceinline__ fp2p_t fp2_3pm2(const fp2p_t& X, const fp2p_t& x, bool minus) {
   return pr_make(fp_3pm2(X.v, x.v, minus));
 }
-#if BLS_FP2_INLINE == 2
-// inlined bodies fenced by scheduling barriers: the scheduler cannot interleave
-// two products, so the live set stays one product's temporaries + the caller's state
-__device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
-  BLS_PHASE();
-  const fp_t r = fp2p_mul_body(a.v, b.v);
-  BLS_PHASE();
-  return pr_make(r);
-}
-__device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) {
-  BLS_PHASE();
-  const fp_t r = fp2p_sqr_body(a.v);
-  BLS_PHASE();
-  return pr_make(r);
-}
-#else
 __device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
   return pr_make(fp_unpack(fp2p_mul_call(fp_pack(a.v), fp_pack(b.v))));
 }
 __device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) { return pr_make(fp_unpack(fp2p_sqr_call(fp_pack(a.v)))); }
-#endif
 __device__ __forceinline__ bool fp2_is_zero(const fp2p_t& a) { return pr_both(fp_is_zero(a.v)); }
 __device__ __forceinline__ bool fp2_eq(const fp2p_t& a, const fp2p_t& b) { return pr_both(fp_eq(a.v, b.v)); }
 

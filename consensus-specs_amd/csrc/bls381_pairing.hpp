@@ -129,12 +129,10 @@ BLS_INLINE fp12_g<E> fp12_mul_by_line_pair_inl(const fp12_g<E>& f, const fp12_g<
   return r;
 }
 
-// BLS_ML_LINE_PAIR=1: miller_loop_n multiplies the lines of pairs k, k+1 together first
-// (23 instead of 26 Fp2 products per step).  Off: on k_miller_verify it measured 14.15 ms
-// against 13.97 ms, same box, alternating runs (the product's live set adds spills).
-#ifndef BLS_ML_LINE_PAIR
-#define BLS_ML_LINE_PAIR 0
-#endif
+// (Round 2 measured multiplying the lines of pairs k, k+1 together first, 23 instead of 26 Fp2
+// products per step, on this loop: 14.15 against 13.97 ms, the product's live set adds spills;
+// the knob BLS_ML_LINE_PAIR was removed in round 6.  The split Miller loop's k_ml_lines / k_ml_accum
+// do form L = l l' -- there each kernel holds only its own half of the state.)
 
 // Multi-Miller loop over n pairs (Q_k affine in G2, P_k affine in G1), all finite.
 // Returns conj(prod_k f_{|x|,Q_k}(P_k)) = prod_k f_{x,Q_k}(P_k) up to factors the
@@ -168,32 +166,14 @@ BLS_NOINLINE ml_result<E> miller_loop_run(const ml_pairs<N, E> in) {
   bool first = true;
   for (int i = 62; i >= 0; --i) {
     if (!first) f = fp12_sqr_inl(f);
-    int k = 0;
-#if BLS_ML_LINE_PAIR
-    for (; k + 1 < N; k += 2) {
-      E c0, c1, c2, d0, d1, d2;
-      line_dbl(T[k], P[k], c0, c1, c2);
-      line_dbl(T[k + 1], P[k + 1], d0, d1, d2);
-      f = fp12_mul_by_line_pair_inl(f, line_pair_product(c0, c1, c2, d0, d1, d2));
-    }
-#endif
-    for (; k < N; ++k) {
+    for (int k = 0; k < N; ++k) {
       E c0, c1, c2;
       line_dbl(T[k], P[k], c0, c1, c2);
       f = fp12_mul_by_line_inl(f, c0, c1, c2);
     }
     first = false;
     if ((BLS_X_ABS >> i) & 1) {
-      k = 0;
-#if BLS_ML_LINE_PAIR
-      for (; k + 1 < N; k += 2) {
-        E c0, c1, c2, d0, d1, d2;
-        line_add(T[k], Q[k], P[k], c0, c1, c2);
-        line_add(T[k + 1], Q[k + 1], P[k + 1], d0, d1, d2);
-        f = fp12_mul_by_line_pair_inl(f, line_pair_product(c0, c1, c2, d0, d1, d2));
-      }
-#endif
-      for (; k < N; ++k) {
+      for (int k = 0; k < N; ++k) {
         E c0, c1, c2;
         line_add(T[k], Q[k], P[k], c0, c1, c2);
         f = fp12_mul_by_line_inl(f, c0, c1, c2);
@@ -329,13 +309,11 @@ BLS_INLINE fp12_g<E> cyc_decompress(const cyc_bc<E>& g, const E& inv4g2) {
 // wave has one, the wave takes the Granger-Scott path instead (uniform branch).
 BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 
-// BLS_CYC_TAIL_GS=1: only the snapshots after 16, 48 and 57 squarings are compressed ones.
-// The last six squarings (runs 3, 2, 1) continue from the decompressed f^(2^57) with
-// Granger-Scott squarings on the full element: three decompressions and their shares of the
-// shared inversion (~30 Fp2 products) against six dearer squarings (~6 x 1.3 Fp2 products).
-#ifndef BLS_CYC_TAIL_GS
-#define BLS_CYC_TAIL_GS 1
-#endif
+// Only the snapshots after 16, 48 and 57 squarings are compressed ones.  The last six
+// squarings (runs 3, 2, 1) continue from the decompressed f^(2^57) with Granger-Scott squarings
+// on the full element: three decompressions and their shares of the shared inversion (~30 Fp2
+// products) against six dearer squarings (~6 x 1.3 Fp2 products).  (r03q: the all-compressed
+// form with six snapshots measured the same time with a 480 B larger frame; removed in r06.)
 
 // BLS_FE_MARK(k): phase marks for tools/fe_phases.hip (no code in the library)
 #ifndef BLS_FE_MARK
@@ -345,19 +323,23 @@ BLS_CONST int CYC_X_RUNS_RTL[6] = {16, 32, 9, 3, 2, 1};
 #define BLS_FE_STEP(j)
 #endif
 
-// BLS_FE_MUL_CALL=1 (measurement knob): the final exponentiation's Fp12 products as calls
-// (fp12_mul, operands through the stack) instead of inlined
-#ifndef BLS_FE_MUL_CALL
-#define BLS_FE_MUL_CALL 0
-#endif
-#if BLS_FE_MUL_CALL
-#define FE_MUL12 fp12_mul
-#else
+// the final exponentiation's Fp12 products are inlined (r04r: as calls, fp12_mul with its
+// operands through the stack, 9.79-9.83 against 9.16-9.20 ms per 2^16 launch)
 #define FE_MUL12 fp12_mul_inl
-#endif
 
-#if BLS_CYC_TAIL_GS
 template <class E>
+BLS_INLINE fp12_g<E> fp12_zero() { fp12_g<E> r; r.c0 = fp6_zero<E>(); r.c1 = fp6_zero<E>(); return r; }
+
+// FB: what a wave does when a snapshot has g2 = 0 (f = 1 from the infinity/infinity verify, or a
+// point of measure zero), where the compressed form cannot be decompressed:
+//   1: the exact Granger-Scott chain cyc_exp_x_gs, in this call (host build, latency kernels);
+//   0: the wave returns 0 instead.  0 propagates through final_exp's chain (every later value is
+//      a product with it, or an exponentiation of it), so final_exp_check reports the wave's items
+//      as to be redone and k_final_exp_redo recomputes them with FB = 1.  The throughput kernel
+//      then has neither cyc_exp_x_gs nor the called fp12_mul it uses in its call tree: the
+//      fallback's 1,360 B + fp12_mul's 2,000 B frames leave every wave's scratch segment
+//      (VERDICT r05 next #2).
+template <class E, int FB = 1>
 BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
   BLS_FE_MARK(7);
   cyc_bc<E> snap[3];
@@ -373,7 +355,10 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
     zero = zero | zs;
   }
   BLS_FE_MARK(0);
-  if (BLS_ANY(zero)) return cyc_exp_x_gs(f);
+  if (BLS_ANY(zero)) {
+    if constexpr (FB != 0) return cyc_exp_x_gs(f);
+    else return fp12_zero<E>();
+  }
   const E d0 = fp2_mul_small(snap[0].g2, 4), d1 = fp2_mul_small(snap[1].g2, 4);
   const E p01 = fp2_mul(d0, d1);
   E inv = fp2_inv(fp2_mul(p01, fp2_mul_small(snap[2].g2, 4)));   // 1 / (d0 d1 d2)
@@ -391,52 +376,45 @@ BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
   }
   return fp12_conj(r);
 }
-#else
-template <class E>
-BLS_NOINLINE fp12_g<E> cyc_exp_x(const fp12_g<E> f) {
-  cyc_bc<E> snap[6];
-  cyc_bc<E> g = cyc_compress(f);
-  bool zero = false;
-  for (int s = 0; s < 6; ++s) {
-    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = cyc_csqr(g);
-    snap[s] = g;
-    const bool zs = fp2_is_zero(g.g2);   // evaluated on both lanes of a pair
-    zero = zero | zs;
-  }
-  if (BLS_ANY(zero)) return cyc_exp_x_gs(f);
-  // prefix products of the denominators 4 g2, one inversion, then back to front
-  E pre[6];
-  pre[0] = fp2_mul_small(snap[0].g2, 4);
-  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(snap[s].g2, 4));
-  E inv = fp2_inv(pre[5]);
-  fp12_g<E> r = fp12_one<E>();
-  for (int s = 5; s >= 0; --s) {
-    const E is = s ? fp2_mul(inv, pre[s - 1]) : inv;
-    if (s) inv = fp2_mul(inv, fp2_mul_small(snap[s].g2, 4));
-    const fp12_g<E> x = cyc_decompress(snap[s], is);
-    r = (s == 5) ? x : FE_MUL12(r, x);
-  }
-  return fp12_conj(r);
-}
-#endif
 
 // f^(3 (q^12 - 1)/r).  3 is coprime to r, so the result is 1 exactly when the
 // reduced pairing value is 1 (DESIGN.md "Final exponentiation").
-// Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3.
-template <class E>
-BLS_HD inline fp12_g<E> final_exp(const fp12_g<E> f) {
+// Hard part: 3 (q^4 - q^2 + 1)/r = (x-1)^2 (x+q) (x^2+q^2-1) + 3, computed as c * t^3 with
+// c = t^((x-1)^2 (x+q) (x^2+q^2-1)) (final_exp_ct returns the two factors).
+template <class E> struct fe_ct { fp12_g<E> c, t3; };
+
+template <class E, int FB = 1>
+BLS_HD inline fe_ct<E> final_exp_ct(const fp12_g<E> f) {
   fp12_g<E> t = FE_MUL12(fp12_conj(f), fp12_inv(f));     // f^(q^6 - 1)
   t = FE_MUL12(fp12_frob(t, 2), t);                     // ^(q^2 + 1)
   BLS_FE_MARK(5);
-  fp12_g<E> a = FE_MUL12(cyc_exp_x(t), fp12_conj(t));     // t^(x-1)
-  a = FE_MUL12(cyc_exp_x(a), fp12_conj(a));            // t^((x-1)^2)
-  const fp12_g<E> b = FE_MUL12(cyc_exp_x(a), fp12_frob(a, 1));            // a^(x+q)
-  const fp12_g<E> bx2 = cyc_exp_x(cyc_exp_x(b));
-  const fp12_g<E> c = FE_MUL12(FE_MUL12(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
-  const fp12_g<E> t3 = FE_MUL12(fp12_cyclotomic_sqr(t), t);
-  const fp12_g<E> res = FE_MUL12(c, t3);
+  fp12_g<E> a = FE_MUL12(cyc_exp_x<E, FB>(t), fp12_conj(t));     // t^(x-1)
+  a = FE_MUL12(cyc_exp_x<E, FB>(a), fp12_conj(a));              // t^((x-1)^2)
+  const fp12_g<E> b = FE_MUL12(cyc_exp_x<E, FB>(a), fp12_frob(a, 1));            // a^(x+q)
+  const fp12_g<E> bx2 = cyc_exp_x<E, FB>(cyc_exp_x<E, FB>(b));
+  fe_ct<E> r;
+  r.c = FE_MUL12(FE_MUL12(bx2, fp12_frob(b, 2)), fp12_conj(b));  // b^(x^2+q^2-1)
+  r.t3 = FE_MUL12(fp12_cyclotomic_sqr(t), t);
   BLS_FE_MARK(6);
-  return res;
+  return r;
+}
+
+template <class E>
+BLS_HD inline fp12_g<E> final_exp(const fp12_g<E> f) {
+  const fe_ct<E> r = final_exp_ct<E, 1>(f);
+  return FE_MUL12(r.c, r.t3);
+}
+
+// The verdict form: 1 when f^(3(q^12-1)/r) == 1, else 0.  c t^3 == 1 is tested as c == conj(t^3)
+// (t^3 is in the cyclotomic subgroup, where the inverse is the conjugate): one Fp12 product
+// fewer than final_exp.  FB = 0 (cyc_exp_x): 2 when the item's wave returned the zero marker,
+// i.e. c = 0 -- tested on two coefficients, so a genuine c with both zero (a measure-zero event)
+// is merely recomputed by the exact launch too.
+template <class E, int FB = 1>
+BLS_HD inline int final_exp_check(const fp12_g<E> f) {
+  const fe_ct<E> r = final_exp_ct<E, FB>(f);
+  if (FB == 0 && fp2_is_zero(r.c.c0.c0) && fp2_is_zero(r.c.c1.c0)) return 2;
+  return fp12_eq(r.c, fp12_conj(r.t3)) ? 1 : 0;
 }
 
 }  // namespace bls381

@@ -818,8 +818,8 @@ __device__ inline fq12_t final_exp_q(const fq12_t f) {
 
 
 // ---- the final exponentiation on an octet, products split (k_final_exp_verdict_oq) ----
-// The compressed squarings stay in the quad form on both quads (the four-way split of
-// cyc_exp_x_o below costs more in exchanges than it saves); every Fp12 product runs its Fp6
+// The compressed squarings stay in the quad form on both quads (BLS381_FE_OCT=2; the default
+// splits them four ways as well, cyc_exp_x_oo below); every Fp12 product runs its Fp6
 // products over the four lane pairs: fq12_mul 9 product steps -> 5.
 // fp6_mul_split with its three products per half split A: 0, 2 | B: 1, 2 (the same values)
 __device__ __forceinline__ fp6p_t fp6_mul_split_oct(const fp6p_t& s, const fp6p_t& t) {
@@ -985,37 +985,6 @@ __device__ __forceinline__ fp2p_t co_sqr(const fp2p_t& g) {
   return pr_make(fp_6p2_3m2(!sq, R, R, g.v));
 }
 
-// cyc_exp_x_q with the squarings on the octet
-__device__ __noinline__ fq12_t cyc_exp_x_o(const fq12_t f) {
-  const bool hi = qd_hi();
-  cq_t snap[6];
-  fp2p_t g = co_enter(cq_compress(f));
-  bool zero = false;
-  for (int s = 0; s < 6; ++s) {
-    for (int j = CYC_X_RUNS_RTL[s]; j > 0; --j) g = co_sqr(g);
-    snap[s] = co_exit(g);
-    zero = zero | fp2_is_zero(cq_g2(snap[s]));
-  }
-  if (BLS_ANY(zero)) return cyc_exp_x_gs_q(f);
-  fp2p_t pre[6];
-  pre[0] = fp2_mul_small(cq_g2(snap[0]), 4);
-  for (int s = 1; s < 6; ++s) pre[s] = fp2_mul(pre[s - 1], fp2_mul_small(cq_g2(snap[s]), 4));
-  fp2p_t inv = fp2_inv(pre[5]);
-  fq12_t r;
-  for (int s = 5; s >= 0; --s) {
-    fp2p_t is = inv;
-    if (s) {
-      const fp2p_t p = fp2_mul(inv, qd_sel(hi, fp2_mul_small(cq_g2(snap[s]), 4), pre[s - 1]));
-      const fp2p_t po = qd_swap(p);
-      is = qd_sel(hi, po, p);
-      inv = qd_sel(hi, p, po);
-    }
-    const fq12_t x = cq_decompress(snap[s], is);
-    r = (s == 5) ? x : fq12_mul(r, x);
-  }
-  return fq12_conj(r);
-}
-
 // cyc_exp_x_oq with the squarings on the octet as well (co_sqr) -- the single-call FE (BLS381_FE_OCT=3)
 __device__ __noinline__ fq12_t cyc_exp_x_oo(const fq12_t f) {
   const bool hi = qd_hi();
@@ -1057,19 +1026,6 @@ __device__ inline fq12_t final_exp_oo(const fq12_t f) {
   const fq12_t c = fq12_mul_oct(fq12_mul_oct(bx2, fq12_frob(b, 2)), fq12_conj(b));
   const fq12_t t3 = fq12_mul_oct(fq12_sqr_oct(t), t);
   return fq12_mul_oct(c, t3);
-}
-
-// final_exp_q with cyc_exp_x_o: both quads of the octet hold f
-__device__ inline fq12_t final_exp_o(const fq12_t f) {
-  fq12_t t = fq12_mul(fq12_conj(f), fq12_inv(f));
-  t = fq12_mul(fq12_frob(t, 2), t);
-  fq12_t a = fq12_mul(cyc_exp_x_o(t), fq12_conj(t));
-  a = fq12_mul(cyc_exp_x_o(a), fq12_conj(a));
-  const fq12_t b = fq12_mul(cyc_exp_x_o(a), fq12_frob(a, 1));
-  const fq12_t bx2 = cyc_exp_x_o(cyc_exp_x_o(b));
-  const fq12_t c = fq12_mul(fq12_mul(bx2, fq12_frob(b, 2)), fq12_conj(b));
-  const fq12_t t3 = fq12_mul(fq12_sqr(t), t);
-  return fq12_mul(c, t3);
 }
 
 }  // namespace bls381

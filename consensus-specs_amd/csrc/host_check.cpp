@@ -118,6 +118,10 @@ void hc_fp12_mul_by_line(const uint8_t* f, const uint8_t* c0, const uint8_t* c1,
   st12(o, fp12_mul_by_line(ld12(f), ld2(c0), ld2(c1), ld2(c2)));
 }
 void hc_final_exp(const uint8_t* a, uint8_t* o) { st12(o, final_exp(ld12(a))); }
+// the verdict form (final_exp_check): 1 / 0, or 2 with fb = 0 when a snapshot had g2 = 0
+int hc_final_exp_check(const uint8_t* a, int fb) {
+  return fb ? final_exp_check<fp2_t, 1>(ld12(a)) : final_exp_check<fp2_t, 0>(ld12(a));
+}
 
 // lax != 0: py_ecc 1.7.0's codec, else the spec's strict one
 int hc_g1_decompress(const uint8_t* b48, uint8_t* aff96, int lax) {
@@ -326,7 +330,7 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   const fp12_t f = miller_loop_n<2>(Q, Pp, degen);
   out[3] = g_fp_macs;
   g_fp_macs = 0;
-  const bool ok = fp12_is_one(final_exp(f));
+  const bool ok = final_exp_check<fp2_t, 1>(f) == 1;   // the kernel's verdict form (one product fewer)
   out[4] = g_fp_macs;
   // the split Miller loop of the throughput path, per kernel (bls381_kernels.hpp):
   // out[5] k_ml_lines (both running points, L = l l'), out[6] k_ml_accum (f^2 L)

@@ -84,6 +84,11 @@ def _outcome(fn, *a):
         return type(e).__name__
 
 
+# out-of-range domain with a bad key in one of two message groups: py_ecc's outcome depends on
+# the order of set(message_hashes) (A.6)
+ORDER_DEPENDENT = ("bad_first_group_domain_2_64", "bad_later_group_domain_2_64")
+
+
 def shim_cases():
     """The boundary's residual py_ecc behaviours (VERDICT r04 missing #4), run through the
     bls shim only (the device batch layouts take fixed 48 / 96-byte records):
@@ -170,6 +175,11 @@ def shim_cases():
             "expected_pyecc": _outcome(o.verify_multiple, pl, ml, s, dd),
             "expected_strict": _outcome(o.verify_multiple_strict, pl, ml, s, dd)})
         c = out["shim_verify_multiple"][-1]
+        if kind in ORDER_DEPENDENT:
+            # py_ecc 1.7.0 walks set(message_hashes), whose order follows the process's hash seed:
+            # it decodes a bad group's keys first (False) or serialises the domain first
+            # (OverflowError).  The oracle and the shim take the sorted order; both outcomes are py_ecc's.
+            c["pyecc_order_dependent"] = [False, "OverflowError"]
         print("shim verify_multiple", kind, c["expected_pyecc"], c["expected_strict"], flush=True)
     aggp = [("leading_zero_bytes", [b"\x00" + p for p in pks]), ("leading_junk_byte", [b"\x5a" + pks[0]]),
             ("empty_key", [b""]), ("short_key", [pks[0][2:]]), ("control", pks)]

@@ -150,9 +150,10 @@ def test_thread_policy_override_is_per_thread():
 
 
 def test_shim_does_not_rewrite_process_policy():
-    """bls.bls_verify scopes its policy to the call: a process-wide 'strict' set by another
-    front end survives a shim call (here one that stops before the device: a wrong length
-    under the shim's strict policy, while the process-wide policy is py_ecc's)."""
+    """bls.bls_verify scopes its policy to the call: the shim's own 'strict' does not leak into
+    the process-wide policy (a call that stops before the device: a wrong length under the
+    shim's strict policy).  The converse -- a process-wide 'strict' surviving a shim call that
+    reaches the device -- is tests/test_gpu_parity.py::test_shim_call_keeps_process_policy."""
     from bls381_amd import _native, bls
     old = bls.SUBGROUP_POLICY
     bls.SUBGROUP_POLICY = "strict"
@@ -173,3 +174,28 @@ def test_rccl_path_resolves_without_a_device():
         pytest.skip("RCCL not loadable: %s" % e)
     assert "rccl" in os.path.basename(p)
     assert os.path.realpath(p) in comm.loaded_rccl_paths()
+
+
+def test_library_has_no_flat_instructions():
+    """VERDICT r05 weak #6 / DESIGN.md section 10.8: no generic (flat) memory access in the shipped
+    gfx950 code object.  Round 5 removed every pointer into a caller's private memory from the
+    call boundaries (by-value operands, force-inlined reference helpers, address_space(1) SoA
+    accessors): a flat access to the private aperture is the fault class of the round-2 max-ilp
+    and round-5 BLS_FP2_INLINE=2 builds.  Static check of lib/libbls381.so (no GPU)."""
+    import subprocess
+    import sys
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    so = os.path.join(ROOT, "consensus-specs_amd", "lib", "libbls381.so")
+    if not os.path.exists(objdump) or not os.path.exists(so):
+        pytest.skip("llvm-objdump or the built library missing")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from extract_co import extract
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        co = os.path.join(d, "bls.co")
+        extract(so, co)
+        dis = subprocess.run([objdump, "-d", "--no-show-raw-insn", co], capture_output=True, text=True,
+                             timeout=300).stdout
+    flat = [ln.strip() for ln in dis.splitlines() if ln.strip().startswith("flat_")]
+    assert "v_mad_u64_u32" in dis          # the disassembly is the engine's
+    assert not flat, "%d flat instructions, e.g. %s" % (len(flat), flat[:3])

@@ -227,6 +227,17 @@ def test_fp12(L):
     # an element of Fp6 (b = 0): the easy part maps it to 1 as well
     g6 = f[:3] + (M.ZERO2,) * 3
     L.hc_final_exp(b576(g6), buf); assert i576(buf.raw) == M.final_exp(g6) == M.ONE12
+    # the verdict form: c == conj(t^3) instead of the last product; without the fallback
+    # (fb = 0, the throughput kernel) a g2 = 0 snapshot reports 2 (k_final_exp_redo's items)
+    fr = M.ONE12
+    for bit in bin(O.r)[2:]:                 # f^r: its final exponentiation is 1
+        fr = M.mul12(fr, fr)
+        if bit == "1":
+            fr = M.mul12(fr, f)
+    for x, want in ((f, 0), (fr, 1)):
+        assert L.hc_final_exp_check(b576(x), 1) == L.hc_final_exp_check(b576(x), 0) == want
+    for x in (M.ONE12, g6):
+        assert L.hc_final_exp_check(b576(x), 1) == 1 and L.hc_final_exp_check(b576(x), 0) == 2
 
 
 def test_codecs_and_subgroups(L, golden):

@@ -237,20 +237,6 @@ def test_sanitized_host_build_over_golden_batches(tmp_path):
     assert "mismatches 0" in res.stdout
 
 
-def test_line_pair_knob_host_build_over_golden_batches(tmp_path):
-    """The off-by-default two-line Miller product (BLS_ML_LINE_PAIR=1):
-    host build of the device headers with the knob on, every golden and torsion case."""
-    import build_native
-    lib = build_native.build_hostcheck(defines=("BLS_ML_LINE_PAIR=1",))
-    runner = tmp_path / "run.py"
-    runner.write_text(_ASAN_RUNNER)
-    g = os.path.join(ROOT, "tests", "golden")
-    res = subprocess.run([sys.executable, str(runner), lib, os.path.join(g, "bls_golden_batches.json"),
-                          os.path.join(g, "bls_torsion.json"), os.path.join(g, "bls_noncanonical.json")],
-                         capture_output=True, text=True, timeout=600)
-    assert res.returncode == 0 and "mismatches 0" in res.stdout, res.stdout[-2000:] + res.stderr[-2000:]
-
-
 def _outcome(fn, *a):
     try:
         return fn(*a)
