@@ -84,7 +84,8 @@ def parse():
                     help="with several ranks: end the secondary lines after this many seconds (the headline is kept)")
     ap.add_argument("--sections", type=str, default="",
                     help="comma list: run only these secondary lines (host, deposits, randomized, c3, c4, c5, rccl, latency)")
-    ap.add_argument("--rb-batch", type=str, default="32", help="randomized sub-batch sizes (comma list)")
+    ap.add_argument("--rb-batch", type=str, default="64,8",
+                    help="randomized sub-batch sizes (comma list; the first is the line's own, r06: 64 the best clean, 8 the best with 1/16 tampered)")
     ap.add_argument("--c4-keys", type=int, default=1 << 17, help="pubkeys per GPU in the C4 aggregation")
     ap.add_argument("--c5", type=str, default="16,128,1024,4096", help="C5 distinct-message counts")
     ap.add_argument("--policy", choices=["pyecc", "strict"], default="pyecc",
@@ -907,7 +908,51 @@ def _bench_randomized_b(native, L, args, pks, msgs, sigs, doms, expected, world,
         t = _max_time(time.perf_counter() - t0, world, dist, dev)
         out[name] = {"verifications_per_s": n * steps * world / t, "ms_per_step": 1e3 * t / steps,
                      "accepted_in_batches": int(st[0]), "verified_singly": int(st[1]), "failed_sub_batches": int(st[2])}
+        if name == "clean":
+            # the path's own roofline: per-kernel HIP-event times from two extra,
+            # untimed steps, and its algorithmic work per item against the clean step's time
+            native.profile_enable(True)
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            prof = native.profile_read()
+            native.profile_enable(False)
+            out["roofline"] = rb_roofline(pks, msgs, sigs, doms, B, n, {k: v["total_ms"] / 2 for k, v in prof.items()},
+                                          1e-3 * out["clean"]["ms_per_step"])
     return out
+
+
+def rb_roofline(pks, msgs, sigs, doms, B, n, kern_ms, step_s):
+    """Algorithmic work of the randomized path (Fp-product equivalents per item, MAC-weighted as the
+    headline's) over the clean step's wall time, and the item Miller accumulation (k_ml_accum_q, its
+    largest kernel) against its own launch time."""
+    import build_native
+    c = count_fp_muls(pks, msgs, sigs, doms)
+    L = ctypes.CDLL(build_native.build_hostcheck(count_ops=True))
+    rb = np.zeros(5)
+    for i in range(4):
+        o = (ctypes.c_uint64 * 5)()
+        if L.hc_count_rb_item(pks[48 * i:48 * i + 48], sigs[96 * i:96 * i + 96], 0x9E3779B9 ^ i, 0x7F4A7C15 + i, o) == 0:
+            rb += np.array(list(o), dtype=float)
+    rb /= 4 * ISSUED_MACS_PER_FP_MUL
+    sig_sum = 15 * rb[2] if B <= 256 else rb[3]   # bucket MSM (2 x 8 windows x 15/16 adds) or the ladder
+    per_item = {"decode_g1": c["decode_g1"], "scale_g1": rb[0], "decode_g2": c["decode_g2"], "g2_test": rb[1],
+                "hash_to_g2": c["hash_to_g2"], "item_miller_lines": c["miller_lines"] / 2,
+                "item_miller_accum": c["miller_accum"] / 2, "signature_sum": sig_sum,
+                "sub_batch_products": 54 * 0.5, "sub_batch_miller": rb[4] / B, "sub_batch_final_exp": c["final_exp"] / B}
+    peak, _ = load_valu_peak()
+    work = sum(per_item.values())
+    whole = work * MACS_PER_FP_MUL * n / step_s / 1e12
+    res = {"fp_mul_per_item": {k: round(v, 1) for k, v in per_item.items()}, "fp_mul_per_item_total": round(work, 1),
+           "default_path_fp_mul_per_item": round(sum(c[k] for k in PIPELINE_STAGES), 1),
+           "pipeline_achieved": round(whole, 3), "pipeline_frac": round(whole / peak, 4) if peak else None,
+           "peak": peak, "unit": "T MAC/s", "kernel_avg_ms": {k: round(v, 3) for k, v in kern_ms.items()}}
+    acc_ms = kern_ms.get("rb_miller_accum")
+    if acc_ms:
+        a = c["miller_accum"] * MACS_PER_FP_MUL * (n / 2) / (1e-3 * acc_ms) / 1e12
+        res["dominant"] = {"kernel": "rb_miller_accum (k_ml_accum_q)", "achieved": round(a, 3),
+                           "frac": round(a / peak, 4) if peak else None}
+    return res
 
 
 def bench_latency(native, pks, msgs, sigs, expected):
