@@ -334,7 +334,7 @@ MAC_PROBE_FILE = os.path.join(ROOT, "profiles", "mac_probe_r05k.txt")
 def mac_stream_ceiling(achieved, peak):
     """The rate a pure v_mad_u64_u32 stream reaches at the verify kernels' occupancy (two waves per
     SIMD, tools/mac_probe.hip, measured once per build round): the ceiling any kernel at that occupancy
-    can approach, beside the issue-bound peak the frac is priced against."""
+    can approach, beside the issue-bound peak the frac is priced against (HISTORY.md, round 5 "What bounds the products")."""
     try:
         rates = []
         block = None

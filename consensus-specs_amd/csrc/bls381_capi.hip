@@ -3028,8 +3028,11 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("agg_g2_affine", sb, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
     HIPC(hipEventRecord(c->ev_join, sb));
     HIPC(hipStreamWaitEvent(c->prio, c->ev_join, 0));
+    // BLS381_RB_SIGPRIO (measurement knob, default 1 under order 2): the sums' loop waves raise their
+    // issue priority (s_setprio 3) beside k_hash_bp
+    static const int sig_prio = env_knob("BLS381_RB_SIGPRIO", 1);
     LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
-           (const uint8_t*)s_st, nslots, f, fst);
+           (const uint8_t*)s_st, nslots, f, fst, order == 2 ? sig_prio : 0);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
     if (order == 2) {
       // the cofactor map beside the sums' Miller loops (which raise their waves' priority)

@@ -121,7 +121,7 @@ template <> struct soa_jac<fp2p_t> {
 // The latency kernels' lane assignment: units (items or pair tasks) of LPI lanes each.  A wave that
 // holds at least one unit keeps all 64 lanes active -- lanes past the last unit recompute it with
 // their stores masked (`live` false) -- and a wave with no unit exits.  Partially filled waves of these
-// spill-heavy kernels ran erratically slower (r05, DESIGN.md section 0: the quad FE took 2.86-3.87 ms
+// spill-heavy kernels ran erratically slower (r05, HISTORY.md round 5: the quad FE took 2.86-3.87 ms
 // with 8 of 64 lanes in use and 2.87-2.91 ms with all 64; 1-item calls 9.3-9.5 against 8.4 ms).
 template <int LPI>
 __device__ __forceinline__ bool lat_unit(size_t n_units, size_t& u, bool& live) {
@@ -1414,10 +1414,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(siz
 __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t slot_per,
                                                          const uint32_t* __restrict__ s_aff,
                                                          const uint8_t* __restrict__ s_st, size_t nslots,
-                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
-  // a few latency-bound waves beside a full-chip launch (k_hash_bp): they win their SIMD's issue
+                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out,
+                                                         int prio) {
+  // prio: a few latency-bound waves beside a full-chip launch (k_hash_bp) win their SIMD's issue
   // arbitration, so the sums' loops end before the item Miller loops need every wave slot
-  __builtin_amdgcn_s_setprio(3);
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const size_t b = item_index<4>();
   if (b >= nb) return;
   const size_t slot = b * (slot_per + 1) + slot_per;

@@ -362,6 +362,44 @@ int hc_count_verify_stages(const uint8_t* pk48, const uint8_t* msg32, const uint
   return ok ? 1 : 0;
 }
 
+// MACs of the randomized path's per-item and per-sub-batch stages (bench.py rb roofline):
+// out[0] [r] pk = sigma(pk) + the joint 32-bit ladder + affine (k_rb_decode_g1's scalar part),
+// out[1] the signature's G2 test (k_rb_g2_test), out[2] one mixed G2 addition (the MSM's unit:
+// ~15 per item at 4-bit windows), out[3] the joint 32-bit G2 ladder [r] sig (k_rb_scale_g2, the
+// path above the MSM's sub-batch cap), out[4] one Miller pair (S, -[c] g1) (k_rb_miller_sig).
+int hc_count_rb_item(const uint8_t* pk48, const uint8_t* sig96, uint32_t k0, uint32_t k1, uint64_t* out) {
+  aff_t<fp_t> P;
+  aff_t<fp2_t> S;
+  if (g1_decompress(P, pk48, true) != PT_OK || g2_decompress(S, sig96, true) != PT_OK) return -1;
+  g_fp_macs = 0;
+  aff_t<fp_t> sp;
+  sp.x = fp_mul(G1_BETA_M, P.x);
+  sp.y = P.y;
+  aff_t<fp_t> r1;
+  jac_to_aff(r1, jac_mul_2x32(P, sp, k0, k1));
+  out[0] = g_fp_macs;
+  g_fp_macs = 0;
+  (void)g2_in_subgroup(S);
+  out[1] = g_fp_macs;
+  g_fp_macs = 0;
+  const jac_t<fp2_t> j = jac_mul_2x32(S, g2_psi(S), 3u, 5u);   // a generic Jacobian point
+  g_fp_macs = 0;
+  (void)jac_add_aff(j, S);
+  out[2] = g_fp_macs;
+  aff_t<fp2_t> sq = g2_psi(g2_psi(S));
+  sq.y = fp2_neg(sq.y);
+  g_fp_macs = 0;
+  (void)jac_mul_2x32(S, sq, k0, k1);
+  out[3] = g_fp_macs;
+  aff_t<fp_t> ng; ng.x = G1_VGEN_X_M; ng.y = G1_VGEN_NEGY_M;
+  const g1_line_pre pre = g1_prepare(ng);
+  bool degen = false;
+  g_fp_macs = 0;
+  (void)miller_loop_n<1>(&S, &pre, degen);
+  out[4] = g_fp_macs;
+  return 0;
+}
+
 // MACs (BLS_COUNT_MACS) of one committee aggregation of n pubkeys (decode + adds)
 int hc_count_aggregate(size_t n, const uint8_t* pks, uint64_t* out) {
   g_fp_macs = 0;

@@ -1,7 +1,7 @@
 // Does a lone wave pay for instruction fetch on long straight-line code?  A v_mad_u64_u32 stream
 // as one straight-line body of BODY instructions (8 bytes each), run ITERS times, against the same
 // number of MACs in a small loop; one wave alone, two or four waves of one workgroup (one CU), and
-// one wave in each of two workgroups.  DESIGN.md section 0 (latency).
+// one wave in each of two workgroups.  HISTORY.md, round 5 (latency).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/icache_probe.hip -o tools/icache_probe
 #include <hip/hip_runtime.h>
 #include <cstdio>
