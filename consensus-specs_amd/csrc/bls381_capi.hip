@@ -411,6 +411,17 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // Default: 4 for py_ecc, 1 for strict.
   static const int c2_order_env = env_knob("BLS381_C2_ORDER", -1);
   const int c2_order = c2_order_env >= 0 ? c2_order_env : (chk ? 1 : 4);
+  // order 4's three one-lane launches as ONE launch whose workgroups take the three roles in turn
+  // (k_prologue_1, r06): the SIMD slots go to the roles in a fixed interleaved order instead of
+  // whichever stream's waves the dispatcher took first.  BLS381_FUSED_PROLOGUE=0: three streams.
+  static const int fused_prologue = env_knob("BLS381_FUSED_PROLOGUE", 1);
+  if (c2_order == 4 && fused_prologue && n > BLS_HASH_WIDE_MAX_N && hash_split() && (g2_one_lane() & 1)) {
+    LAUNCH("prologue", s, dim3(3 * grid_for(n)), b, k_prologue_1<0>, n, pks, sigs, msgs, (uint32_t)32, doms, 8,
+           (const uint8_t*)nullptr, w.pk_aff, w.pk_st, w.sig_aff, w.sig_st, w.h_aff, (uint32_t*)nullptr,
+           (uint8_t*)nullptr, policy_flags(chk), policy_flags(sig_in_loop ? 0 : chk));
+    LAUNCH("hash_bp", s, g2, b, k_hash_bp, n, w.h_aff, (uint8_t*)nullptr);
+    return run_verify_pairings(n, w, verdicts, s, sig_in_loop);
+  }
   hipStream_t sd = c2_order ? c->side : s;
   HIPC(hipEventRecord(c->ev_fork, s));
   HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
@@ -2964,15 +2975,21 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     //  2 (default, r06): the default path's order-4 prologue -- k_rb_decode_g1 (decode + [r_i] pk_i)
     //    on the side stream, the codec-only k_decode_g2_1 on the second side stream and the
     //    hash's one-lane k_hash_cand_1 on the main stream share the chip; then the signatures' G2
-    //    test + item classes (k_rb_g2_test, lane pairs) and the signature sums; the sums' Miller
-    //    loops on the high-priority stream beside k_hash_bp, then the item Miller loops.
+    //    test + item classes (k_rb_g2_test, lane pairs); the signature branch (sums, affine, the sums'
+    //    Miller loops) on the priority stream beside k_hash_bp and the item Miller loops.
     //  0 (round 5): decode_g1, decode_g2 with the G2 test (pairs) and the signature sums in
     //    sequence on the main stream, the sums' Miller loops on the high-priority stream beside
     //    hash_to_G2 (pair kernel) and [r_i] pk_i (k_rb_scale_g1).
     std::lock_guard<std::mutex> lk(c->fork_mu);
     static const int order = env_knob("BLS381_RB_ORDER", 2);
     hipStream_t sb = s;
-    if (order == 2) {
+    static const int fused_prologue = env_knob("BLS381_FUSED_PROLOGUE", 1);
+    if (order == 2 && fused_prologue) {
+      // the three one-lane roles in one launch (k_prologue_1<1>, as in the default path)
+      LAUNCH("rb_prologue", s, dim3(3 * grid_for(n)), blk, k_prologue_1<1>, n, pks, sigs, msgs, (uint32_t)32, doms, 8,
+             (const uint8_t*)d_seed, w.pk_aff, w.pk_st, w.sig_aff, w.sig_st, w.h_aff, r1, r1_st, policy_flags(chk),
+             policy_flags(0));
+    } else if (order == 2) {
       HIPC(hipEventRecord(c->ev_fork, s));
       HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
       HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
@@ -2984,8 +3001,16 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
       LAUNCH("hash_cand", s, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
       HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
       HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
+    }
+    if (order == 2) {
       LAUNCH("rb_g2_test", s, g2, blk, k_rb_g2_test, n, (const uint32_t*)w.sig_aff, w.sig_st, (const uint8_t*)w.pk_st,
              cls, chk);
+      // the whole signature branch (sums, their affine form, their Miller loops) on the priority
+      // stream beside k_hash_bp and the item Miller loops: its window and combine chains and the
+      // sums' loops are latency-bound launches of a few waves each
+      HIPC(hipEventRecord(c->ev_fork, s));
+      HIPC(hipStreamWaitEvent(c->prio, c->ev_fork, 0));
+      sb = c->prio;
     } else {
       LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
       // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
@@ -3028,14 +3053,13 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("agg_g2_affine", sb, dim3(grid_for(2 * nb)), blk, k_agg_g2_affine, nb, sjac, sbad, s_aff, s_st);
     HIPC(hipEventRecord(c->ev_join, sb));
     HIPC(hipStreamWaitEvent(c->prio, c->ev_join, 0));
-    // BLS381_RB_SIGPRIO (measurement knob, default 1 under order 2): the sums' loop waves raise their
-    // issue priority (s_setprio 3) beside k_hash_bp
-    static const int sig_prio = env_knob("BLS381_RB_SIGPRIO", 1);
+    // (r06: the sums' loop waves at raised issue priority, s_setprio 3, slowed k_hash_bp beside them
+    // from 3.6 to 5.4 ms: 2.47 against 2.60 M/s at B = 64, same box; removed)
     LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
-           (const uint8_t*)s_st, nslots, f, fst, order == 2 ? sig_prio : 0);
+           (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
     if (order == 2) {
-      // the cofactor map beside the sums' Miller loops (which raise their waves' priority)
+      // the cofactor map beside the signature branch
       LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
     } else {
       LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,

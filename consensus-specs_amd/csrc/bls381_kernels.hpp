@@ -150,10 +150,9 @@ __device__ __forceinline__ size_t item_index() {
 
 // --------------------------------------------------------- decode kernels --
 // pubkeys -> affine G1 (SoA 2 Fp) + status; optional subgroup check
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
-                                                     uint32_t* __restrict__ out, uint8_t* __restrict__ st,
-                                                     int check_subgroup) {
-  const size_t i = item_index<1>();
+__device__ __forceinline__ void dev_decode_g1(size_t i, size_t n, const uint8_t* __restrict__ pks,
+                                              uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                              int check_subgroup) {
   if (i >= n) return;
   uint8_t b[48];
   ld_bytes(b, pks + 48 * i, 48);
@@ -162,6 +161,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n
   if (s == PT_OK && (check_subgroup & CHK_SUB_MASK) && !g1_in_subgroup(a)) s = PT_BAD;
   st[i] = (uint8_t)s;
   if (s == PT_OK) soa_st_g1(out, n, i, a);
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g1(size_t n, const uint8_t* __restrict__ pks,
+                                                     uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                     int check_subgroup) {
+  dev_decode_g1(item_index<1>(), n, pks, out, st, check_subgroup);
 }
 
 // signatures -> affine G2 (pair SoA, 2 Fp2) + status; check_subgroup: 0 none,
@@ -251,10 +255,9 @@ __device__ __forceinline__ void soa_st_g2_1(uint32_t* p, size_t n, size_t i, con
   soa_st(p, 2 * n, 2 * i, 0, a.x.c0); soa_st(p, 2 * n, 2 * i + 1, 0, a.x.c1);
   soa_st(p, 2 * n, 2 * i, 1, a.y.c0); soa_st(p, 2 * n, 2 * i + 1, 1, a.y.c1);
 }
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t n, const uint8_t* __restrict__ sigs,
-                                                       uint32_t* __restrict__ out, uint8_t* __restrict__ st,
-                                                       int check_subgroup) {
-  const size_t i = item_index<1>();
+__device__ __forceinline__ void dev_decode_g2_1(size_t i, size_t n, const uint8_t* __restrict__ sigs,
+                                                uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                int check_subgroup) {
   if (i >= n) return;
   aff_t<fp2_t> a;
   const int sub = check_subgroup & CHK_SUB_MASK;
@@ -262,6 +265,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t
   if (s == PT_OK && sub && !g2_in_subgroup(a)) s = sub == 2 ? ST_NOSUB : PT_BAD;
   st[i] = (uint8_t)s;
   if (s == PT_OK || s == ST_NOSUB) soa_st_g2_1(out, n, i, a);
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_decode_g2_1(size_t n, const uint8_t* __restrict__ sigs,
+                                                       uint32_t* __restrict__ out, uint8_t* __restrict__ st,
+                                                       int check_subgroup) {
+  dev_decode_g2_1(item_index<1>(), n, sigs, out, st, check_subgroup);
 }
 
 // hash_to_G2 in two launches (the throughput path): the try-and-increment search and the
@@ -297,10 +305,9 @@ __device__ __forceinline__ uint32_t lane_shfl(uint32_t v, uint32_t src) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
 }
 
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_cand_1(size_t n, const uint8_t* __restrict__ msgs,
-                                                       uint32_t mlen, const uint8_t* __restrict__ doms,
-                                                       int dom_stride, uint32_t* __restrict__ out) {
-  const size_t i = item_index<1>();
+__device__ __forceinline__ void dev_hash_cand_1(size_t i, size_t n, const uint8_t* __restrict__ msgs, uint32_t mlen,
+                                                const uint8_t* __restrict__ doms, int dom_stride,
+                                                uint32_t* __restrict__ out) {
 #if BLS_HASH_COMPACT
   // every lane of the wave takes part in the pooled search: no early return before it
   const bool valid = i < n;
@@ -367,6 +374,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_cand_1(size_t
   hash_to_g2_candidate(c, msgs + (size_t)mlen * i, mlen, dom);
   soa_st_g2_1(out, n, i, c);
 #endif
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_cand_1(size_t n, const uint8_t* __restrict__ msgs,
+                                                       uint32_t mlen, const uint8_t* __restrict__ doms,
+                                                       int dom_stride, uint32_t* __restrict__ out) {
+  dev_hash_cand_1(item_index<1>(), n, msgs, mlen, doms, dom_stride, out);
 }
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_hash_bp(size_t n, uint32_t* __restrict__ pts,
                                                    uint8_t* __restrict__ st) {
@@ -1159,12 +1171,11 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t
 // k_rb_decode_g1: one lane per item; the pubkey decoded under the call's codec and subgroup mode
 // (as k_decode_g1), and for a finite key R1 = [r_i] pk_i affine (status OK / INF).  The class waits
 // for the signature's G2 test (k_rb_g2_test).
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_t n, const uint8_t* __restrict__ pks,
-                                                        const uint8_t* __restrict__ seed32,
-                                                        uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st,
-                                                        uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
-                                                        int check_subgroup) {
-  const size_t i = item_index<1>();
+__device__ __forceinline__ void dev_rb_decode_g1(size_t i, size_t n, const uint8_t* __restrict__ pks,
+                                                 const uint8_t* __restrict__ seed32,
+                                                 uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st,
+                                                 uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
+                                                 int check_subgroup) {
   if (i >= n) return;
   uint8_t b[48];
   ld_bytes(b, pks + 48 * i, 48);
@@ -1186,6 +1197,38 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_
     }
   }
   r1_st[i] = st;
+}
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_t n, const uint8_t* __restrict__ pks,
+                                                        const uint8_t* __restrict__ seed32,
+                                                        uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st,
+                                                        uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
+                                                        int check_subgroup) {
+  dev_rb_decode_g1(item_index<1>(), n, pks, seed32, pk_aff, pk_st, r1_aff, r1_st, check_subgroup);
+}
+
+// The one-lane prologue as ONE launch (r06): workgroup b takes role b % 3 -- the hash's search + root,
+// the pubkey decode (RB: + [r_i] pk_i), the signature decode -- over the items of workgroup b / 3, so
+// the dispatcher hands every CU (and every XCD: b % 8) the three roles interleaved in a fixed order.
+// As three launches on three streams the order in which their waves took the SIMD slots varied from
+// step to step: when the decodes' waves came first the hash search waited for slots and the prologue
+// took 3.2-3.7 ms instead of 2.8-2.9 (profiles/timeline_c2_r06c.txt).
+template <int RB>
+__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_prologue_1(
+    size_t n, const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
+    uint32_t mlen, const uint8_t* __restrict__ doms, int dom_stride, const uint8_t* __restrict__ seed32,
+    uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st, uint32_t* __restrict__ sig_aff,
+    uint8_t* __restrict__ sig_st, uint32_t* __restrict__ h_aff, uint32_t* __restrict__ r1_aff,
+    uint8_t* __restrict__ r1_st, int chk_g1, int chk_g2) {
+  const uint32_t role = blockIdx.x % 3u;
+  const size_t i = (size_t)(blockIdx.x / 3u) * blockDim.x + threadIdx.x;
+  if (role == 0) {
+    dev_hash_cand_1(i, n, msgs, mlen, doms, dom_stride, h_aff);
+  } else if (role == 1) {
+    if (RB) dev_rb_decode_g1(i, n, pks, seed32, pk_aff, pk_st, r1_aff, r1_st, chk_g1);
+    else dev_decode_g1(i, n, pks, pk_aff, pk_st, chk_g1);
+  } else {
+    dev_decode_g2_1(i, n, sigs, sig_aff, sig_st, chk_g2);
+  }
 }
 
 // k_rb_g2_test: one lane pair per item; the signature's G2 membership (psi(Q) == [x] Q) after the
@@ -1414,11 +1457,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(siz
 __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_miller_sig(size_t nb, size_t slot_per,
                                                          const uint32_t* __restrict__ s_aff,
                                                          const uint8_t* __restrict__ s_st, size_t nslots,
-                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out,
-                                                         int prio) {
-  // prio: a few latency-bound waves beside a full-chip launch (k_hash_bp) win their SIMD's issue
-  // arbitration, so the sums' loops end before the item Miller loops need every wave slot
-  if (prio) __builtin_amdgcn_s_setprio(3);
+                                                         uint32_t* __restrict__ f_out, uint8_t* __restrict__ st_out) {
   const size_t b = item_index<4>();
   if (b >= nb) return;
   const size_t slot = b * (slot_per + 1) + slot_per;
