@@ -1206,12 +1206,13 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_
   dev_rb_decode_g1(item_index<1>(), n, pks, seed32, pk_aff, pk_st, r1_aff, r1_st, check_subgroup);
 }
 
-// The one-lane prologue as ONE launch (r06): workgroup b takes role b % 3 -- the hash's search + root,
-// the pubkey decode (RB: + [r_i] pk_i), the signature decode -- over the items of workgroup b / 3, so
-// the dispatcher hands every CU (and every XCD: b % 8) the three roles interleaved in a fixed order.
-// As three launches on three streams the order in which their waves took the SIMD slots varied from
-// step to step: when the decodes' waves came first the hash search waited for slots and the prologue
-// took 3.2-3.7 ms instead of 2.8-2.9 (profiles/timeline_c2_r06c.txt).
+// The one-lane prologue as ONE launch (r06): the workgroups take the three roles in dispatch order --
+// first the hash's search + root (the longest), then the pubkey decode (RB: + [r_i] pk_i), then the
+// signature decode, nb workgroups each.  As three launches on three streams the order in which their
+// waves took the SIMD slots varied from step to step: with the hash search first the prologue took
+// 2.8-2.9 ms, with the pubkey decode first the search waited for slots and it took 3.2-3.7 ms
+// (profiles/prologue_spans_r06c.txt).  Interleaving the roles (workgroup b: role b % 3) measured
+// 3.17-3.19 ms (r06d); this order fixes the fast one.
 template <int RB>
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_prologue_1(
     size_t n, const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
@@ -1219,8 +1220,9 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_prologue_1(
     uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st, uint32_t* __restrict__ sig_aff,
     uint8_t* __restrict__ sig_st, uint32_t* __restrict__ h_aff, uint32_t* __restrict__ r1_aff,
     uint8_t* __restrict__ r1_st, int chk_g1, int chk_g2) {
-  const uint32_t role = blockIdx.x % 3u;
-  const size_t i = (size_t)(blockIdx.x / 3u) * blockDim.x + threadIdx.x;
+  const uint32_t nb = gridDim.x / 3u;
+  const uint32_t role = blockIdx.x / nb;
+  const size_t i = (size_t)(blockIdx.x - role * nb) * blockDim.x + threadIdx.x;
   if (role == 0) {
     dev_hash_cand_1(i, n, msgs, mlen, doms, dom_stride, h_aff);
   } else if (role == 1) {
