@@ -411,11 +411,12 @@ int run_verify_batch(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, 
   // Default: 4 for py_ecc, 1 for strict.
   static const int c2_order_env = env_knob("BLS381_C2_ORDER", -1);
   const int c2_order = c2_order_env >= 0 ? c2_order_env : (chk ? 1 : 4);
-  // order 4's three one-lane launches as ONE launch whose workgroups take the three roles in turn
-  // (k_prologue_1, r06): the SIMD slots go to the roles in a fixed interleaved order instead of
-  // whichever stream's waves the dispatcher took first.  BLS381_FUSED_PROLOGUE=0: three streams.
-  static const int fused_prologue = env_knob("BLS381_FUSED_PROLOGUE", 1);
-  if (c2_order == 4 && fused_prologue && n > BLS_HASH_WIDE_MAX_N && hash_split() && (g2_one_lane() & 1)) {
+  // order 4's three one-lane launches as ONE launch whose workgroups take the three roles in dispatch
+  // order, the hash search first (k_prologue_1, r06): as three streams the SIMD slots went to whichever
+  // stream's waves the dispatcher took first, and the prologue took 2.8-2.9 or 3.2-3.7 ms from step to
+  // step (profiles/prologue_spans_r06c.txt); fused 2.9-3.0 on a box where the three streams ran 0.9-1.9 %
+  // slower per step (profiles/bench_r06e_*.json, alternating)
+  if (c2_order == 4 && n > BLS_HASH_WIDE_MAX_N && hash_split() && (g2_one_lane() & 1)) {
     LAUNCH("prologue", s, dim3(3 * grid_for(n)), b, k_prologue_1<0>, n, pks, sigs, msgs, (uint32_t)32, doms, 8,
            (const uint8_t*)nullptr, w.pk_aff, w.pk_st, w.sig_aff, w.sig_st, w.h_aff, (uint32_t*)nullptr,
            (uint8_t*)nullptr, policy_flags(chk), policy_flags(sig_in_loop ? 0 : chk));
@@ -2964,58 +2965,30 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
   uint8_t* fst = b.take<uint8_t>(nslots);
   uint32_t* mlL = b.take<uint32_t>(ML_L_WORDS_PER_ITEM * ch_ml);
   uint8_t* mlst = b.take<uint8_t>(ch_ml);
-  // per sub-batch sum of [r_i] sig_i (planned here; runs on the side stream)
+  // per sub-batch sum of [r_i] sig_i (planned here; runs on the priority stream)
   std::vector<uint32_t> off(nb + 1);
   for (size_t k = 0; k <= nb; ++k) off[k] = (uint32_t)std::min(n, k * B);
   auto plan = std::make_shared<AggPlan>(plan_agg(nb, off.data()));
   uint32_t* s_aff = b.take<uint32_t>(4 * FP_LIMBS * nb);
   uint8_t* s_st = b.take<uint8_t>(nb);
   {
-    // Order, BLS381_RB_ORDER (measurement knob):
-    //  2 (default, r06): the default path's order-4 prologue -- k_rb_decode_g1 (decode + [r_i] pk_i)
-    //    on the side stream, the codec-only k_decode_g2_1 on the second side stream and the
-    //    hash's one-lane k_hash_cand_1 on the main stream share the chip; then the signatures' G2
-    //    test + item classes (k_rb_g2_test, lane pairs); the signature branch (sums, affine, the sums'
-    //    Miller loops) on the priority stream beside k_hash_bp and the item Miller loops.
-    //  0 (round 5): decode_g1, decode_g2 with the G2 test (pairs) and the signature sums in
-    //    sequence on the main stream, the sums' Miller loops on the high-priority stream beside
-    //    hash_to_G2 (pair kernel) and [r_i] pk_i (k_rb_scale_g1).
+    // Order: the one-lane prologue as one launch (k_prologue_1<1>: the hash's
+    // search + root, decode + [r_i] pk_i, the codec-only signature decode), then the signatures' G2
+    // test and the item classes (k_rb_g2_test, lane pairs); the signature branch (sums, their affine
+    // form, their Miller loops) on the priority stream beside k_hash_bp and the item Miller loops.
+    // Round 5's order (decode_g1, decode_g2 with the G2 test and the sums in sequence, then the pair
+    // hash and k_rb_scale_g1) measured 2.36 against 2.43-2.53 M/s (r06b); removed.
     std::lock_guard<std::mutex> lk(c->fork_mu);
-    static const int order = env_knob("BLS381_RB_ORDER", 2);
-    hipStream_t sb = s;
-    static const int fused_prologue = env_knob("BLS381_FUSED_PROLOGUE", 1);
-    if (order == 2 && fused_prologue) {
-      // the three one-lane roles in one launch (k_prologue_1<1>, as in the default path)
-      LAUNCH("rb_prologue", s, dim3(3 * grid_for(n)), blk, k_prologue_1<1>, n, pks, sigs, msgs, (uint32_t)32, doms, 8,
-             (const uint8_t*)d_seed, w.pk_aff, w.pk_st, w.sig_aff, w.sig_st, w.h_aff, r1, r1_st, policy_flags(chk),
-             policy_flags(0));
-    } else if (order == 2) {
-      HIPC(hipEventRecord(c->ev_fork, s));
-      HIPC(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-      HIPC(hipStreamWaitEvent(c->side2, c->ev_fork, 0));
-      LAUNCH("rb_decode_g1", c->side, g1, blk, k_rb_decode_g1, n, pks, (const uint8_t*)d_seed, w.pk_aff, w.pk_st, r1,
-             r1_st, policy_flags(chk));
-      HIPC(hipEventRecord(c->ev_join, c->side));
-      LAUNCH("decode_g2_1", c->side2, g1, blk, k_decode_g2_1, n, sigs, w.sig_aff, w.sig_st, policy_flags(0));
-      HIPC(hipEventRecord(c->ev_join3, c->side2));
-      LAUNCH("hash_cand", s, g1, blk, k_hash_cand_1, n, msgs, (uint32_t)32, doms, 8, w.h_aff);
-      HIPC(hipStreamWaitEvent(s, c->ev_join, 0));
-      HIPC(hipStreamWaitEvent(s, c->ev_join3, 0));
-    }
-    if (order == 2) {
-      LAUNCH("rb_g2_test", s, g2, blk, k_rb_g2_test, n, (const uint32_t*)w.sig_aff, w.sig_st, (const uint8_t*)w.pk_st,
-             cls, chk);
-      // the whole signature branch (sums, their affine form, their Miller loops) on the priority
-      // stream beside k_hash_bp and the item Miller loops: its window and combine chains and the
-      // sums' loops are latency-bound launches of a few waves each
-      HIPC(hipEventRecord(c->ev_fork, s));
-      HIPC(hipStreamWaitEvent(c->prio, c->ev_fork, 0));
-      sb = c->prio;
-    } else {
-      LAUNCH("decode_g1", sb, g1, blk, k_decode_g1, n, pks, w.pk_aff, w.pk_st, policy_flags(chk));
-      // every signature's subgroup is needed: outside G2 it is ST_BAD (strict) or ST_NOSUB (py_ecc: single path)
-      LAUNCH("decode_g2", sb, g2, blk, k_decode_g2, n, sigs, w.sig_aff, w.sig_st, policy_flags(chk ? 1 : 2));
-    }
+    LAUNCH("rb_prologue", s, dim3(3 * grid_for(n)), blk, k_prologue_1<1>, n, pks, sigs, msgs, (uint32_t)32, doms, 8,
+           (const uint8_t*)d_seed, w.pk_aff, w.pk_st, w.sig_aff, w.sig_st, w.h_aff, r1, r1_st, policy_flags(chk),
+           policy_flags(0));
+    LAUNCH("rb_g2_test", s, g2, blk, k_rb_g2_test, n, (const uint32_t*)w.sig_aff, w.sig_st, (const uint8_t*)w.pk_st,
+           cls, chk);
+    // the signature branch's window and combine chains and the sums' loops are latency-bound
+    // launches of a few waves each: beside the full-chip ones on the main stream
+    HIPC(hipEventRecord(c->ev_fork, s));
+    HIPC(hipStreamWaitEvent(c->prio, c->ev_fork, 0));
+    hipStream_t sb = c->prio;
     // BLS381_RB_MSM (measurement knob): 1 (default) the sub-batch sums sum_i [r_i] sig_i as one bucket
     // MSM per sub-batch (k_rb_msm_*); 0 a joint 32-bit ladder per item (k_rb_scale_g2) and a tree sum
     // The MSM gives each (sub-batch, window, digit) bucket to one lane pair, which adds its ~B/16
@@ -3058,15 +3031,8 @@ int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* m
     LAUNCH("rb_miller_sig", c->prio, dim3(grid_for(4 * nb)), blk, k_rb_miller_sig, nb, hb, (const uint32_t*)s_aff,
            (const uint8_t*)s_st, nslots, f, fst);
     HIPC(hipEventRecord(c->ev_join2, c->prio));
-    if (order == 2) {
-      // the cofactor map beside the signature branch
-      LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
-    } else {
-      LAUNCH("hash_to_g2", s, g2, blk, k_hash_g2, n, msgs, (uint32_t)32, doms, 8, w.h_aff, w.f_st,
-             (const uint32_t*)nullptr, 0);
-      LAUNCH("rb_scale_g1", sb, g1, blk, k_rb_scale_g1, n, (const uint8_t*)d_seed, (const uint32_t*)w.pk_aff,
-             (const uint8_t*)w.pk_st, (const uint8_t*)w.sig_st, r1, r1_st, cls);
-    }
+    // the cofactor map beside the signature branch
+    LAUNCH("hash_bp", s, g2, blk, k_hash_bp, n, w.h_aff, w.f_st);
     // the batched items two per Miller accumulator: lines of both pairs on a quad, then f^2 L
     // on quads (2^15 accumulators per 2^16 items: a pair launch would leave SIMDs half empty)
     const size_t nq = nb * hb;

@@ -1137,38 +1137,10 @@ __device__ __forceinline__ rb_weight rb_scalar(const uint8_t* seed32, uint64_t i
   return w;
 }
 
-// per item, one lane: its class, and R1 = [r_i] pk_i affine (status OK / INF)
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g1(size_t n, const uint8_t* __restrict__ seed32,
-                                                       const uint32_t* __restrict__ pk_aff,
-                                                       const uint8_t* __restrict__ pk_st,
-                                                       const uint8_t* __restrict__ sig_st,
-                                                       uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
-                                                       uint8_t* __restrict__ cls) {
-  const size_t i = item_index<1>();
-  if (i >= n) return;
-  const uint8_t ps = pk_st[i], ss = sig_st[i];
-  const uint8_t c = (ps == ST_BAD || ss == ST_BAD) ? RB_BAD : (ss == ST_NOSUB ? RB_SINGLE : RB_BATCH);
-  cls[i] = c;
-  uint8_t st = ST_INF;
-  if (c == RB_BATCH && ps == ST_OK) {
-    const aff_t<fp_t> p = soa_ld_g1(pk_aff, n, i);
-    aff_t<fp_t> sp;                       // sigma(p) = [-x^2] p
-    sp.x = fp_mul(G1_BETA_M, p.x);
-    sp.y = p.y;
-    const rb_weight w = rb_scalar(seed32, i);
-    aff_t<fp_t> a;
-    if (jac_to_aff(a, jac_mul_2x32(p, sp, w.k0, w.k1))) {
-      soa_st_g1(r1_aff, n, i, a);
-      st = ST_OK;
-    }
-  }
-  r1_st[i] = st;
-}
-
-// The randomized prologue (round 6), in the default path's order-4 shape: three one-lane
-// launches share the chip -- k_rb_decode_g1 (decode + [r_i] pk_i), k_decode_g2_1 (codec only)
-// and the hash's k_hash_cand_1 -- then the pair launches k_hash_bp and k_rb_g2_test.
-// k_rb_decode_g1: one lane per item; the pubkey decoded under the call's codec and subgroup mode
+// The randomized prologue (round 6), in the default path's shape: the one-lane roles -- decode +
+// [r_i] pk_i (dev_rb_decode_g1), the codec-only signature decode and the hash's search + root -- in
+// one launch (k_prologue_1<1>), then the pair launches k_rb_g2_test and k_hash_bp.
+// dev_rb_decode_g1: one lane per item; the pubkey decoded under the call's codec and subgroup mode
 // (as k_decode_g1), and for a finite key R1 = [r_i] pk_i affine (status OK / INF).  The class waits
 // for the signature's G2 test (k_rb_g2_test).
 __device__ __forceinline__ void dev_rb_decode_g1(size_t i, size_t n, const uint8_t* __restrict__ pks,
@@ -1197,13 +1169,6 @@ __device__ __forceinline__ void dev_rb_decode_g1(size_t i, size_t n, const uint8
     }
   }
   r1_st[i] = st;
-}
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_decode_g1(size_t n, const uint8_t* __restrict__ pks,
-                                                        const uint8_t* __restrict__ seed32,
-                                                        uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st,
-                                                        uint32_t* __restrict__ r1_aff, uint8_t* __restrict__ r1_st,
-                                                        int check_subgroup) {
-  dev_rb_decode_g1(item_index<1>(), n, pks, seed32, pk_aff, pk_st, r1_aff, r1_st, check_subgroup);
 }
 
 // The one-lane prologue as ONE launch (r06): the workgroups take the three roles in dispatch order --
@@ -1252,7 +1217,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_g2_test(size_t 
 
 // per item, one lane pair: R2 = [r_i] sig_i (Jacobian SoA; infinity when the item is not
 // batched: a bad pubkey, or a signature that is not a finite point of G2 -- the class
-// k_rb_scale_g1 assigns, recomputed from the statuses so this branch needs no cls)
+// k_rb_g2_test assigns, recomputed from the statuses)
 __global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_rb_scale_g2(size_t n, const uint8_t* __restrict__ seed32,
                                                        const uint32_t* __restrict__ sig_aff,
                                                        const uint8_t* __restrict__ sig_st,
