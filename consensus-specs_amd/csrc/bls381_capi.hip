@@ -184,6 +184,33 @@ constexpr size_t FPW = 4 * FP_LIMBS;   // bytes per Fp element in SoA buffers
 
 unsigned grid_for(size_t n, int block = KBLOCK) { return (unsigned)((n + block - 1) / block); }
 
+// The clock-based wave balance (bls381_pair.hpp, BLS_WAVE_BALANCE=2) runs in a launch with no LDS
+// allocation; launch() gives every other launch 256 B of dynamic LDS (no kernel reads it) as the
+// switch, which the device tests with one s_getreg.  Balanced: launches that put two waves on every
+// SIMD, all resident from the start (CUs x 4 SIMDs x 64 < lanes <= CUs x 4 x 2 x 64) -- in a
+// longer launch a finished wave's slot takes the next wave, in a smaller one a SIMD holds one --
+// outside a NoBalanceScope.  The randomized path opens one: its hash and item Miller loops share
+// SIMDs with the signature branch on another stream, which the balance would delay (B = 64:
+// 2.59-2.63 M/s with it against 2.70-2.71, profiles/ab_r06o_balance.txt).
+thread_local bool g_no_balance = false;
+struct NoBalanceScope {
+  bool prev;
+  NoBalanceScope() : prev(g_no_balance) { g_no_balance = true; }
+  ~NoBalanceScope() { g_no_balance = prev; }
+};
+unsigned balance_lds(dim3 grid, dim3 block) {
+  static const size_t simds = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    return (size_t)cus * 4;
+  }();
+  const size_t lanes = (size_t)grid.x * grid.y * grid.z * block.x * block.y * block.z;
+  const bool on = !g_no_balance && lanes > simds * 64 && lanes <= simds * 128;
+  return on ? 0u : 256u;
+}
+
 template <class K, class... A>
 int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... args) {
   if (grid.x == 0) return 0;
@@ -194,7 +221,7 @@ int launch(const char* name, hipStream_t s, dim3 grid, dim3 block, K kern, A... 
     HIPC(hipEventCreate(&ev.b));
     HIPC(hipEventRecord(ev.a, s));
   }
-  hipLaunchKernelGGL(kern, grid, block, 0, s, args...);
+  hipLaunchKernelGGL(kern, grid, block, balance_lds(grid, block), s, args...);
   HIPC(hipGetLastError());
   if (prof) {
     HIPC(hipEventRecord(ev.b, s));
@@ -2946,6 +2973,7 @@ size_t rb_ws_size(size_t n, size_t B) {
 int run_verify_randomized(Ctx* c, size_t n, const uint8_t* pks, const uint8_t* msgs, const uint8_t* sigs,
                           const uint8_t* doms, const uint8_t* seed32, size_t B, uint8_t* d_verdicts, void* ws,
                           size_t ws_cap, hipStream_t s, uint64_t* stats) {
+  const NoBalanceScope no_balance;
   const size_t nb = (n + B - 1) / B, hb = B / 2, nslots = rb_slots(n, B), ch_ml = rb_ml_chunk(n, B);
   Bump b(ws, ws_cap);
   VerifyWs w = carve_verify(b.take<uint8_t>(verify_ws_size(n, false)), n, false);

@@ -44,6 +44,13 @@ constexpr int KBLOCK = 128;   // lanes per workgroup for the per-item kernels
 #ifndef BLS_FE_WAVES_PER_EU
 #define BLS_FE_WAVES_PER_EU BLS_WAVES_PER_EU
 #endif
+// the fused C2 prologue (k_prologue_1<0>): 3 waves per SIMD (168 VGPRs; scratch 5,040 -> 5,808 B/lane)
+// measured 2.68 ms against 2.90 ms at 2 (profiles/ab_r06h_prologue_waves.txt, same box, alternating):
+// its one-lane code is latency-bound, and a third wave hides more than the larger frame costs.
+// The randomized prologue (k_prologue_1<1>) does not fit 3 and stays at BLS_WAVES_PER_EU.
+#ifndef BLS_PROLOGUE_WAVES_PER_EU
+#define BLS_PROLOGUE_WAVES_PER_EU 3
+#endif
 // aggregation kernels (k_agg_chunks, k_agg_lanes): measurement knob
 #ifndef BLS_AGG_WAVES_PER_EU
 #define BLS_AGG_WAVES_PER_EU BLS_WAVES_PER_EU
@@ -629,7 +636,7 @@ __device__ __noinline__ g2_proj<fp2p_t> ml_lines_run_lds(const ml_src src, const
   const g1_dbl_lds dp{col};
   int j = 0;
   for (int b = 62; b >= 0; --b) {
-    wave_balance((unsigned)b);
+    wave_balance_lds((unsigned)b);   // col: LDS
     fp2p_t c0, c1, c2, o0, o1, o2;
     line_dbl(T, dp, c0, c1, c2);
     quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
@@ -1179,7 +1186,7 @@ __device__ __forceinline__ void dev_rb_decode_g1(size_t i, size_t n, const uint8
 // (profiles/prologue_spans_r06c.txt).  Interleaving the roles (workgroup b: role b % 3) measured
 // 3.17-3.19 ms (r06d); this order fixes the fast one.
 template <int RB>
-__global__ void __launch_bounds__(KBLOCK, BLS_WAVES_PER_EU) k_prologue_1(
+__global__ void __launch_bounds__(KBLOCK, RB ? BLS_WAVES_PER_EU : BLS_PROLOGUE_WAVES_PER_EU) k_prologue_1(
     size_t n, const uint8_t* __restrict__ pks, const uint8_t* __restrict__ sigs, const uint8_t* __restrict__ msgs,
     uint32_t mlen, const uint8_t* __restrict__ doms, int dom_stride, const uint8_t* __restrict__ seed32,
     uint32_t* __restrict__ pk_aff, uint8_t* __restrict__ pk_st, uint32_t* __restrict__ sig_aff,

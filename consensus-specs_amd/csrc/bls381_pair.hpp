@@ -21,24 +21,66 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-// BLS_WAVE_BALANCE=1 (default): the two waves a SIMD holds alternate their issue priority (s_setprio)
-// step by step in the Miller accumulation, the line loop and the final exponentiation's squarings.
-// Without it the older wave takes most issue slots and finishes first, and the younger runs its
-// remaining third alone at a lone wave's issue rate (tools/fe_phases.hip: in k_final_exp_verdict's
-// shape the older wave of every SIMD ends at 6.0 ms, the younger at 9.6).  r04y, one box, three
-// alternating rounds: 2.254-2.260 -> 2.268-2.279 M/s (k_ml_accum 7.21-7.23 -> 7.06-7.12 ms).
+// Issue priority of the two waves a SIMD holds (s_setprio).  Without it the older wave takes most
+// issue slots and finishes first, and the younger runs the rest of its work alone at a lone wave's
+// issue rate: in k_final_exp_verdict's shape the older wave of every SIMD ends at 6.2 ms, the
+// younger at 9.4 (tools/fe_phases.hip, profiles/fe_balance_r06.txt).
+//   BLS_WAVE_BALANCE=2 (default, round 6): in a launch that puts two waves on every SIMD, all resident
+//     from the start (one round of two-wave slots), the priority alternates with the real-time clock
+//     (windows of 2^BLS_BALANCE_SHIFT ticks of s_memrealtime's 100 MHz), so both waves hold it for
+//     equal times: 8.5 / 9.0 ms.  It is updated at every lane-pair Fp2 product call and at the
+//     loops' steps.  The host picks those launches (bls381_capi.hip, balance_lds) and marks every
+//     other one with an LDS allocation, which the device reads with one s_getreg; those keep the
+//     step-parity form of 1 at the loops' steps.  Same box, alternating (profiles/ab_r06p_balance.txt):
+//     C2 +1.0 to +2.3 %; k_final_exp_verdict 8.79-8.94 -> 8.45-8.51 ms, k_ml_accum 6.88-6.96 ->
+//     6.61-6.64, k_hash_bp 3.27-3.31 -> 3.19; k_ml_lines, which is never balanced, 6.03-6.08 ->
+//     6.32-6.38 (its loop function's allocation around the calls came out with more spill traffic).
+//   BLS_WAVE_BALANCE=1 (round 4): alternate by step parity at the loops' steps only.  It does not
+//     balance: a wave one step ahead has the same priority as the other, which the older wins.
 #ifndef BLS_WAVE_BALANCE
-#define BLS_WAVE_BALANCE 1
+#define BLS_WAVE_BALANCE 2
+#endif
+#ifndef BLS_BALANCE_SHIFT
+#define BLS_BALANCE_SHIFT 14
 #endif
 namespace bls381 {
-__device__ __forceinline__ void wave_balance(unsigned step) {
-#if BLS_WAVE_BALANCE
-  // the wave's slot on its SIMD (HW_ID[3:0]); a scalar branch, since s_setprio ignores exec
-  const unsigned slot = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) & 1u;
-  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)((step + slot) & 1u));
+__device__ __forceinline__ unsigned wave_slot() {
+  return (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4) & 1u;   // HW_ID[3:0]: the wave's slot
+}
+// s_setprio ignores exec: the condition is made wave-uniform and the branch is a scalar one
+__device__ __forceinline__ void wave_prio(unsigned x) {
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)((x + wave_slot()) & 1u));
   if (hi) __builtin_amdgcn_s_setprio(2); else __builtin_amdgcn_s_setprio(0);
+}
+__device__ __forceinline__ bool wave_has_lds() {
+  return ((unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 6) >> 12) & 0x1ffu;   // HW_REG_LDS_ALLOC size
+}
+__device__ __forceinline__ unsigned balance_clock() {
+  return (unsigned)(__builtin_amdgcn_s_memrealtime() >> BLS_BALANCE_SHIFT);
+}
+// at a loop step
+__device__ __forceinline__ void wave_balance(unsigned step) {
+#if BLS_WAVE_BALANCE == 2
+  if (!wave_has_lds()) wave_prio(balance_clock());
+  else wave_prio(step);
+#elif BLS_WAVE_BALANCE == 1
+  wave_prio(step);
 #else
   (void)step;
+#endif
+}
+// at a loop step of a kernel that always has an LDS allocation (the line loop): the step-parity form
+__device__ __forceinline__ void wave_balance_lds(unsigned step) {
+#if BLS_WAVE_BALANCE
+  wave_prio(step);
+#else
+  (void)step;
+#endif
+}
+// at an Fp2 product call
+__device__ __forceinline__ void wave_balance_call() {
+#if BLS_WAVE_BALANCE == 2
+  if (!wave_has_lds()) wave_prio(balance_clock());
 #endif
 }
 }  // namespace bls381
@@ -129,9 +171,13 @@ __device__ __forceinline__ fp_t fp2p_sqr_body(const fp_t& a) {
 // Both knobs were removed in round 6.
 #define BLS_FP2_CALL __device__ __attribute__((noinline))
 BLS_FP2_CALL fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
+  wave_balance_call();
   return fp_pack(fp2p_mul_body(fp_unpack(a), fp_unpack(b)));
 }
-BLS_FP2_CALL fpv_t fp2p_sqr_call(fpv_t a) { return fp_pack(fp2p_sqr_body(fp_unpack(a))); }
+BLS_FP2_CALL fpv_t fp2p_sqr_call(fpv_t a) {
+  wave_balance_call();
+  return fp_pack(fp2p_sqr_body(fp_unpack(a)));
+}
 
 // ------------------------------------------------------------ Fp2 on a pair --
 __device__ __forceinline__ fp2p_t pr_make(const fp_t& v) { fp2p_t r; r.v = v; return r; }

@@ -373,13 +373,15 @@ def test_batch_against_oracle_small(native):
 
 
 @pytest.mark.parametrize("policy", ["pyecc", "strict"])
-@pytest.mark.parametrize("n", [100, 8193, 12000, 20000, (1 << 18) + 3])
+@pytest.mark.parametrize("n", [100, 8193, 12000, 20000, 60000, (1 << 18) + 3])
 def test_verify_layouts_tiled_special_cases(native, golden, torsion, policy, n):
     """The golden and torsion bls_verify cases (infinite keys and signatures, bad encodings,
     small-order components, a degenerate Miller loop) tiled to n items, so every Miller /
     final-exponentiation layout sees them: n <= 8192 one quad per Miller pair + the 2-value
-    quad FE, n <= 49152 both pairs on one quad + the quad FE, above that lane pairs (2^18 + 3:
-    launches of several rounds of waves with a ragged last wave).  From 8,193 items on the py_ecc
+    quad FE, n <= 49152 both pairs on one quad + the quad FE, above that lane pairs (60,000: the
+    FE, the cofactor map and the Miller accumulation are one-round launches of two waves per
+    SIMD, which run with the clock-based wave balance; 2^18 + 3: launches of several rounds of
+    waves with a ragged last wave).  From 8,193 items on the py_ecc
     policy runs the one-launch prologue (k_prologue_1: each of its three roles ends in a ragged
     workgroup at 8,193).  The tiled verdicts equal the untiled batch's, which equal the fixtures'
     column for the policy."""
