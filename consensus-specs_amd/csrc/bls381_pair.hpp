@@ -28,7 +28,7 @@
 //   BLS_WAVE_BALANCE=2 (default, round 6): in a launch that puts two waves on every SIMD, all resident
 //     from the start (one round of two-wave slots), the priority alternates with the real-time clock
 //     (windows of 2^BLS_BALANCE_SHIFT ticks of s_memrealtime's 100 MHz), so both waves hold it for
-//     equal times: 8.5 / 9.0 ms.  It is updated at every lane-pair Fp2 product call and at the
+//     equal times: 8.5 / 9.0 ms.  It is updated before every lane-pair Fp2 product call and at the
 //     loops' steps.  The host picks those launches (bls381_capi.hip, balance_lds) and marks every
 //     other one with an LDS allocation, which the device reads with one s_getreg; those keep the
 //     step-parity form of 1 at the loops' steps.  Same box, alternating (profiles/ab_r06p_balance.txt):
@@ -171,11 +171,9 @@ __device__ __forceinline__ fp_t fp2p_sqr_body(const fp_t& a) {
 // Both knobs were removed in round 6.
 #define BLS_FP2_CALL __device__ __attribute__((noinline))
 BLS_FP2_CALL fpv_t fp2p_mul_call(fpv_t a, fpv_t b) {
-  wave_balance_call();
   return fp_pack(fp2p_mul_body(fp_unpack(a), fp_unpack(b)));
 }
 BLS_FP2_CALL fpv_t fp2p_sqr_call(fpv_t a) {
-  wave_balance_call();
   return fp_pack(fp2p_sqr_body(fp_unpack(a)));
 }
 
@@ -222,9 +220,15 @@ __device__ __forceinline__ fp2p_t fp2_3pm2(const fp2p_t& X, const fp2p_t& x, boo
   return pr_make(fp_3pm2(X.v, x.v, minus));
 }
 __device__ __forceinline__ fp2p_t fp2_mul(const fp2p_t& a, const fp2p_t& b) {
+  // at the call site, not in the callee: k_final_exp_verdict 8.42-8.54 -> 8.31-8.33 ms, its scratch
+  // frame 7,824 -> 7,440 B/lane (profiles/ab_r06q_balance_site.txt)
+  wave_balance_call();
   return pr_make(fp_unpack(fp2p_mul_call(fp_pack(a.v), fp_pack(b.v))));
 }
-__device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) { return pr_make(fp_unpack(fp2p_sqr_call(fp_pack(a.v)))); }
+__device__ __forceinline__ fp2p_t fp2_sqr(const fp2p_t& a) {
+  wave_balance_call();
+  return pr_make(fp_unpack(fp2p_sqr_call(fp_pack(a.v))));
+}
 __device__ __forceinline__ bool fp2_is_zero(const fp2p_t& a) { return pr_both(fp_is_zero(a.v)); }
 __device__ __forceinline__ bool fp2_eq(const fp2p_t& a, const fp2p_t& b) { return pr_both(fp_eq(a.v, b.v)); }
 
