@@ -1163,6 +1163,36 @@ def test_native_comm_rccl_world1(native, golden, torsion, noncanon):
     assert comm.size() == 0
 
 
+@pytest.mark.parametrize("virtual", [False, True])
+def test_native_comm_destroy_after_device_call(native, virtual):
+    """bls381_comm_destroy right after the device-resident aggregation, with its collectives still
+    queued on the caller's stream and no synchronisation in between: the destroy waits
+    for them, and the aggregate and status written afterwards are the right ones."""
+    import torch
+    from bls381_amd import comm
+    keys = [O.privtopub(k) for k in range(1, 41)]
+    blob = b"".join(keys[i % 40] for i in range(4096))
+    want = O.privtopub(sum((i % 40) + 1 for i in range(4096)))
+    d_pks = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    d_out = torch.zeros(48, dtype=torch.uint8, device="cuda")
+    d_st = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+    if virtual:
+        comm.init_virtual(3)
+    else:
+        comm.init(1, 0, comm.unique_id())
+    try:
+        d_ws = torch.empty(comm.aggregate_pubkeys_device_workspace_size(4096), dtype=torch.uint8, device="cuda")
+        s = torch.cuda.current_stream()
+        comm.aggregate_pubkeys_device(4096, d_pks.data_ptr(), d_out.data_ptr(), d_st.data_ptr(), d_ws.data_ptr(),
+                                      s.cuda_stream)
+    finally:
+        comm.destroy()
+    assert comm.size() == 0
+    torch.cuda.synchronize()
+    assert int(d_st.item()) == 0
+    assert bytes(d_out.cpu().numpy()) == want
+
+
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_native_comm_virtual_ranks(native, golden, torsion, noncanon, world):
     """N ranks on one GPU (bls381_comm_init_virtual): per-rank partials by distinct message,
