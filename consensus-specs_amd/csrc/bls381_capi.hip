@@ -198,7 +198,7 @@ struct NoBalanceScope {
   NoBalanceScope() : prev(g_no_balance) { g_no_balance = true; }
   ~NoBalanceScope() { g_no_balance = prev; }
 };
-unsigned balance_lds(dim3 grid, dim3 block) {
+size_t chip_simds() {
   static const size_t simds = [] {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -206,6 +206,10 @@ unsigned balance_lds(dim3 grid, dim3 block) {
       cus = 256;
     return (size_t)cus * 4;
   }();
+  return simds;
+}
+unsigned balance_lds(dim3 grid, dim3 block) {
+  const size_t simds = chip_simds();
   const size_t lanes = (size_t)grid.x * grid.y * grid.z * block.x * block.y * block.z;
   const bool on = !g_no_balance && lanes > simds * 64 && lanes <= simds * 128;
   return on ? 0u : 256u;
@@ -536,9 +540,17 @@ int run_verify_pairings(size_t n, const VerifyWs& w, uint8_t* verdicts, hipStrea
     const size_t ch = verify_split_chunk(n);
     for (size_t i0 = 0; i0 < n; i0 += ch) {
       const size_t cnt = std::min(ch, n - i0);
-      LAUNCH("miller_lines", s, dim3(grid_for(4 * cnt)), b, k_ml_lines, n, i0, cnt, (const uint32_t*)w.sig_aff,
-             (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
-             w.ml_L, w.ml_st, sig_in_loop ? 1 : 0);
+      // the line loop in launches of at most one round of two-wave slots on quads (CUs x 4 x 32
+      // items), each balanced by the clock when it fills the chip (its static LDS keeps the generic
+      // switch off; the launch passes it instead)
+      const size_t part = chip_simds() * 32;
+      for (size_t l0 = 0; l0 < cnt; l0 += part) {
+        const size_t lc = std::min(part, cnt - l0);
+        const int bal = (!g_no_balance && 4 * lc > chip_simds() * 64) ? 1 : 0;
+        LAUNCH("miller_lines", s, dim3(grid_for(4 * lc)), b, k_ml_lines, n, i0, cnt, (const uint32_t*)w.sig_aff,
+               (const uint8_t*)w.sig_st, (const uint32_t*)w.pk_aff, (const uint8_t*)w.pk_st, (const uint32_t*)w.h_aff,
+               w.ml_L, w.ml_st, sig_in_loop ? 1 : 0, l0, lc, bal);
+      }
       // (r05: the accumulation on lane quads, k_ml_accum_q, measured 8.09-8.18 against 6.96-7.00 ms)
       LAUNCH("miller_accum", s, dim3(grid_for(2 * cnt)), b, k_ml_accum, n, i0, cnt, (const uint32_t*)w.ml_L,
              (const uint8_t*)w.ml_st, w.f, w.f_st, (size_t)0);

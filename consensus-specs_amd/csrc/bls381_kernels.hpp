@@ -624,8 +624,11 @@ __device__ __forceinline__ void ml_lds_put(lds_u32* col, const g1_line_pre& pre)
 // src by value: the L stores cannot alias it (a by-reference src would be re-read from the
 // caller's frame after every store)
 // (the final running point is returned by value: no pointer into the caller's frame)
+// bal: the launch is one round of two-wave slots (the host's choice, bls381_capi.hip): the
+// steps alternate the priority by the clock (BLS_WAVE_BALANCE=2), else by step parity
 __device__ __noinline__ g2_proj<fp2p_t> ml_lines_run_lds(const ml_src src, const lds_u32* col, bool active,
-                                                        uint32_t* __restrict__ L, size_t cnt, size_t li) {
+                                                        uint32_t* __restrict__ L, size_t cnt, size_t li,
+                                                        int bal) {
   const bool hi = qd_hi();
   const fp2p_t one = e2_one<fp2p_t>(), zero = e2_zero<fp2p_t>();
   g2_proj<fp2p_t> T;
@@ -636,7 +639,13 @@ __device__ __noinline__ g2_proj<fp2p_t> ml_lines_run_lds(const ml_src src, const
   const g1_dbl_lds dp{col};
   int j = 0;
   for (int b = 62; b >= 0; --b) {
-    wave_balance_lds((unsigned)b);   // col: LDS
+#if BLS_WAVE_BALANCE == 2
+    if (bal) wave_prio(balance_clock());
+    else wave_balance_lds((unsigned)b);
+#else
+    (void)bal;
+    wave_balance_lds((unsigned)b);
+#endif
     fp2p_t c0, c1, c2, o0, o1, o2;
     line_dbl(T, dp, c0, c1, c2);
     quad_line_pair(qd_sel(active, c0, one), qd_sel(active, c1, zero), qd_sel(active, c2, zero), o0, o1, o2);
@@ -665,9 +674,10 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
                                                     const uint8_t* __restrict__ pk_st,
                                                     const uint32_t* __restrict__ h_aff,
                                                     uint32_t* __restrict__ L, uint8_t* __restrict__ st_out,
-                                                    int sig_check) {
-  const size_t li = item_index<4>();
-  if (li >= cnt) return;
+                                                    int sig_check, size_t l0, size_t lcnt, int bal) {
+  // this launch: items l0 .. l0 + lcnt - 1 of the chunk (L strided by the chunk's cnt)
+  const size_t li = l0 + item_index<4>();
+  if (li >= l0 + lcnt || li >= cnt) return;
   const size_t i = i0 + li;
   const bool hi = qd_hi();
   const bool lead = (threadIdx.x & 3u) == 0;
@@ -686,7 +696,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_ml_lines(size_t
   lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
   const ml_src src{qsrc, 2 * n, lp, use_pk ? pk_aff : nullptr, n, i};
   ml_lds_put(col, g1_prepare(ml_src_p(src)));   // each lane writes and reads only its own column
-  T = ml_lines_run_lds(src, col, active, L, cnt, li);
+  T = ml_lines_run_lds(src, col, active, L, cnt, li, bal);
   const aff_t<fp2p_t> Q = ml_src_q(src);
 #else
   aff_t<fp2p_t> Q;
@@ -1411,7 +1421,7 @@ __global__ void __launch_bounds__(KBLOCK, BLS_ML_WAVES_PER_EU) k_rb_ml_lines(siz
   lds_u32* col = (lds_u32*)lds_pre + threadIdx.x;
   const ml_src src{h_aff, 2 * n, lp, r1_aff, n, i};
   ml_lds_put(col, g1_prepare(ml_src_p(src)));
-  T = ml_lines_run_lds(src, col, active, L, cnt, lq);
+  T = ml_lines_run_lds(src, col, active, L, cnt, lq, 0);
 #else
   aff_t<fp2p_t> Q;
   Q.x = pr_make(soa_ld(h_aff, 2 * n, lp, 0));

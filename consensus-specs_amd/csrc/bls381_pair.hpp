@@ -33,8 +33,10 @@
 //     other one with an LDS allocation, which the device reads with one s_getreg; those keep the
 //     step-parity form of 1 at the loops' steps.  Same box, alternating (profiles/ab_r06p_balance.txt):
 //     C2 +1.0 to +2.3 %; k_final_exp_verdict 8.79-8.94 -> 8.45-8.51 ms, k_ml_accum 6.88-6.96 ->
-//     6.61-6.64, k_hash_bp 3.27-3.31 -> 3.19; k_ml_lines, which is never balanced, 6.03-6.08 ->
-//     6.32-6.38 (its loop function's allocation around the calls came out with more spill traffic).
+//     6.61-6.64, k_hash_bp 3.27-3.31 -> 3.19; k_ml_lines 6.03-6.08 -> 6.32-6.38 (its loop function's
+//     allocation around the calls came out with more spill traffic).  k_ml_lines has static LDS, so
+//     the switch is off in it; its launches are one round each and pass the choice as an argument
+//     (bls381_kernels.hpp, ml_lines_run_lds).
 //   BLS_WAVE_BALANCE=1 (round 4): alternate by step parity at the loops' steps only.  It does not
 //     balance: a wave one step ahead has the same priority as the other, which the older wins.
 #ifndef BLS_WAVE_BALANCE
