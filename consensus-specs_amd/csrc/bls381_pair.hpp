@@ -42,8 +42,10 @@
 #ifndef BLS_WAVE_BALANCE
 #define BLS_WAVE_BALANCE 2
 #endif
+// 2^16 ticks = 655 us: against 2^14 (164 us), same box, C2 -0.2 to +2.3 %, k_ml_lines 6.21-6.32 ->
+// 6.05-6.16 ms, FE 8.38-8.42 -> 8.27-8.33 (profiles/ab_r06st_balance_window.txt; 2^13 and 2^15 too)
 #ifndef BLS_BALANCE_SHIFT
-#define BLS_BALANCE_SHIFT 14
+#define BLS_BALANCE_SHIFT 16
 #endif
 namespace bls381 {
 __device__ __forceinline__ unsigned wave_slot() {
